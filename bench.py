@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""bench.py — IVF-PQ search throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): SIFT1M-shaped synthetic
+data (d=128, 1M base, 100k train, 10,240 queries; clustered, integer-valued
+float32), IndexIVFPQ "IVF1024,PQ16" (8-bit codes) trained on the GPU, nprobe=16,
+k=10, query batch 1024.  One *step* = one whole search of one 1024-query batch
+(coarse probe + inner-product table + fused LUT/scan/top-k) with the queries
+already resident in HBM.
+
+N > 1 (one process per GPU, torch.distributed over RCCL): the index is sharded
+by inverted-list range; the global batch is 1024 x N queries (weak scaling: the
+code bytes each GPU scans per step stay constant), every rank scans its lists
+for the whole batch and an all_to_all returns each query slice's partials to
+its owner, which merges them on the GPU.  ``--mode replicas`` instead runs N
+independent full replicas.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+``roofline`` (the scan kernel's algorithmic code bytes / its HIP-event-timed
+duration against 8 TB/s) and ``cpu_baseline`` (the oracle's Faiss-1.7.1-order
+C restatement, OpenMP over queries, on a bounded sample of the same queries).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "chameleon-rag-acceleration_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--batch", type=int, default=1024)
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--nprobe", type=int, default=16)
+    p.add_argument("--nlist", type=int, default=1024)
+    p.add_argument("--M", type=int, default=16)
+    p.add_argument("--d", type=int, default=128)
+    p.add_argument("--nb", type=int, default=1_000_000)
+    p.add_argument("--nt", type=int, default=100_000)
+    p.add_argument("--nbatches", type=int, default=10)
+    p.add_argument("--niter", type=int, default=25)
+    p.add_argument("--mode", choices=["shard", "replicas"], default="shard")
+    p.add_argument("--cpu-sample", type=int, default=2048, help="queries in the CPU-baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-recall", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_scan_pmc.json"))
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import faiss_amd as faiss
+    from faiss_amd import datasets
+    from faiss_amd.sharding import balanced_list_ranges, exchange_partials
+
+    t_setup = time.time()
+    shard = world > 1 and args.mode == "shard"
+    B = args.batch
+    Bg = B * world if shard else B  # queries per step on each rank
+    log(f"rank {rank}/{world} generating data nb={args.nb} nt={args.nt}")
+    xt = datasets.synthetic_sift_like(args.nt, args.d, seed=4321)
+    xb = datasets.synthetic_sift_like(args.nb, args.d, seed=1234)
+    nq_total = args.nbatches * Bg
+    xq = datasets.synthetic_sift_like(nq_total, args.d, seed=123 + (0 if shard else rank))
+
+    ix = faiss.index_factory(args.d, f"IVF{args.nlist},PQ{args.M}", device=local_rank)
+    ix.niter_coarse = ix.niter_pq = args.niter
+    t0 = time.time()
+    ix.train(xt)
+    log(f"trained in {time.time() - t0:.1f}s")
+    lo, hi = 0, args.nlist
+    if shard:
+        # balance list ranges by code bytes: assign the base set once (top-1)
+        ix.nprobe = 1
+        sizes = np.zeros(args.nlist, np.int64)
+        for i0 in range(0, args.nb, 1 << 18):
+            xbd = torch.from_numpy(xb[i0:i0 + (1 << 18)]).to(dev)
+            _, Iq = ix.coarse_device(xbd)
+            sizes += np.bincount(Iq[:, 0].cpu().numpy(), minlength=args.nlist)
+        lo, hi = balanced_list_ranges(sizes, world, args.M)[rank]
+        ix.set_list_range(lo, hi)
+    t0 = time.time()
+    ix.add(xb)
+    log(f"added {ix.ntotal} vectors (lists [{lo},{hi})) in {time.time() - t0:.1f}s")
+    ix.nprobe = args.nprobe
+    list_sizes = ix.invlists.list_sizes()
+
+    xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
+    k = args.k
+    Dbuf = torch.empty((Bg, k), dtype=torch.float32, device=dev)
+    Ibuf = torch.empty((Bg, k), dtype=torch.int64, device=dev)
+
+    # algorithmic bytes of the scan per batch (codes of every probed list in this rank's range)
+    bytes_alg = []
+    for b in range(args.nbatches):
+        _, Iq = ix.coarse_device(xq_dev[b])
+        Iq = Iq.cpu().numpy()
+        n_codes = list_sizes[Iq].sum()  # lists outside [lo, hi) have size 0 here
+        bytes_alg.append(int(n_codes) * args.M)
+
+    merged = {}
+
+    def step(b):
+        if shard:
+            Dp, Ip = ix.search_device(xq_dev[b], k, Dbuf, Ibuf)
+            Ds, Is = exchange_partials(Dp, Ip, world)
+            merged[b] = faiss.merge_topk_device(Ds, Is)
+        else:
+            ix.search_device(xq_dev[b], k, Dbuf, Ibuf)
+
+    for w in range(args.warmup):
+        step(w % args.nbatches)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    log(f"setup {time.time() - t_setup:.1f}s; timing {args.steps} steps")
+
+    ix.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(s % args.nbatches)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ix.set_timing(False)
+    stages = ix.get_timing()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    queries = args.steps * B * world  # all ranks together
+    qps = queries / elapsed
+    ms_per_step = elapsed * 1000.0 / args.steps
+    scan_ms, scan_n = stages["scan"]
+    scan_avg_ms = scan_ms / max(scan_n, 1)
+    bytes_per_launch = sum(bytes_alg[s % args.nbatches] for s in range(args.steps)) / args.steps
+    achieved = bytes_per_launch / (scan_avg_ms * 1e-3) / 1e9
+
+    # ---------------------------------------------------------- recall (rank 0)
+    recall = None
+    cpu_baseline = None
+    if rank == 0 and not args.no_recall:
+        log("recall: exact float64 ground truth on the GPU")
+        allI = []
+        for b in range(args.nbatches):
+            if shard:
+                continue
+            D, I = ix.search_device(xq_dev[b], k)
+            allI.append(I.cpu().numpy())
+        if allI:
+            I_gpu = np.concatenate(allI)
+            xb64 = torch.from_numpy(xb).to(dev, torch.float64)
+            nb2 = (xb64 * xb64).sum(1)
+            gt = []
+            for i0 in range(0, I_gpu.shape[0], 256):
+                q = torch.from_numpy(xq[i0:i0 + 256]).to(dev, torch.float64)
+                dd = (q * q).sum(1, keepdim=True) + nb2[None, :] - 2.0 * (q @ xb64.T)
+                gt.append(torch.topk(dd, k, dim=1, largest=False).indices.cpu().numpy())
+            gt = np.concatenate(gt)
+            del xb64, nb2
+            r1 = datasets.recall_1_at(I_gpu, gt, (1, k))
+            recall = {"R1@1": r1.get(1), f"R1@{k}": r1.get(k), f"R@{k}": datasets.recall_at_k(I_gpu, gt, k),
+                      "queries": int(I_gpu.shape[0]), "gt": "exact float64 brute force"}
+
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            log("cpu baseline: oracle on a bounded sample")
+            ox = O.OracleIVFPQ(args.d, args.nlist, args.M)
+            ox.set_trained(ix.centroids(), ix.codebook())
+            for l in range(args.nlist):
+                ox.list_ids[l] = ix.invlists.get_ids(l)
+                ox.list_codes[l] = ix.invlists.get_codes(l).reshape(-1, args.M)
+            ox.ntotal = ix.ntotal
+            ox.nprobe = args.nprobe
+            ns = min(args.cpu_sample, nq_total)
+            threads = O.default_threads()
+            ox.search(xq[:64], k, threads)  # warm
+            t0 = time.perf_counter()
+            Dc, Ic = ox.search(xq[:ns], k, threads)
+            tc = time.perf_counter() - t0
+            agree = None
+            if not shard:
+                Ig = np.concatenate([ix.search(xq[i0:i0 + B], k)[1] for i0 in range(0, ns, B)])
+                agree = float((Ig == Ic).mean())
+            cpu_baseline = {"value": ns / tc, "unit": "queries/s", "cores": threads, "kind": "port",
+                            "sample": f"{ns} of the same queries, k={k}, nprobe={args.nprobe}, "
+                                      f"same trained index; oracle/ivfpq_oracle.c (Faiss-1.7.1 order), "
+                                      f"OpenMP over queries, {tc:.2f}s",
+                            "gpu_id_agreement": agree}
+
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            pm = json.load(open(args.pmc_json))
+            if pm.get("config_key") == f"{args.nlist}-{args.M}-{args.nprobe}-{k}-{B}-{world}":
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "queries/sec + recall@10, SIFT1M IVF-PQ (nlist=1024, M=16, nprobe=16)",
+            "value": qps,
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (SIFT1M-shaped clustered integer-valued float32, seeds base 1234 / train 4321 / "
+                    "queries 123); index trained on the GPU",
+            "config": {
+                "workload": f"IVF{args.nlist},PQ{args.M}x8 search, d={args.d}, nb={args.nb}, nprobe={args.nprobe}, "
+                            f"k={k}, batch={B} queries per GPU per step",
+                "parallelism": (f"list-range shards x{world} + RCCL all_to_all merge" if shard
+                                else f"replicas x{world}" if world > 1 else "single GPU"),
+                "global_batch": B * world,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "kernel": "k_scan_topk<16,1> (fused LUT + PQ scan + top-k)",
+                "alg_bytes_per_launch": bytes_per_launch,
+                "avg_launch_ms": scan_avg_ms,
+            },
+            "stages_ms_per_step": {s: v[0] / max(v[1], 1) for s, v in stages.items()},
+            "recall": recall,
+            "cpu_baseline": cpu_baseline,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,907 @@
+// Host side of libivfpq.so: the index object behind the C-ABI of include/ivfpq.h.
+//
+// Owns the trained quantizers and inverted lists on the host (insertion
+// order per list, as Faiss ArrayInvertedLists) and their device images in
+// HBM, and drives the gfx950 kernels of ivfpq_kernels.hip.  Training and
+// encoding run on the GPU; only the k-means centroid update (a per-cluster
+// double-precision mean) and list bookkeeping run on the host.
+//
+// HBM layout (DESIGN.md §Data layout):
+//   centroids f32[nlist][d], |c|^2 f32[nlist], codebook f32[M][256][d/M],
+//   T1 f32[nlist][M][256] (Faiss precomputed_table), codes u8[ntotal][M]
+//   with lists concatenated in list order, ids i64[ntotal] alongside,
+//   list offsets i64[nlist+1].
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "ivfpq.h"
+#include "ivfpq_kernels.h"
+
+using namespace chivf;
+
+namespace {
+
+thread_local std::string g_err;
+
+#define HIPCHECK(x)                                                                          \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+void require(bool ok, const std::string& msg) {
+  if (!ok) throw std::runtime_error(msg);
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t b) {
+    if (b <= bytes && p) return;
+    release();
+    if (b == 0) b = 16;
+    HIPCHECK(hipMalloc(&p, b));
+    bytes = b;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+};
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    HIPCHECK(hipGetDevice(&prev));
+    if (prev != dev) HIPCHECK(hipSetDevice(dev));
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Same generator and update rule as the oracle (oracle/ivfpq_oracle.c,
+// or_rand_perm_prefix / or_kmeans_update) so GPU-trained and oracle-trained
+// indexes are identical for identical input.
+uint64_t splitmix(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+std::vector<int64_t> rand_perm_prefix(int64_t n, int64_t k, uint64_t seed) {
+  std::vector<int64_t> p(n), out(k);
+  for (int64_t i = 0; i < n; i++) p[i] = i;
+  uint64_t s = seed;
+  for (int64_t i = 0; i < k; i++) {
+    int64_t j = i + (int64_t)(splitmix(&s) % (uint64_t)(n - i));
+    std::swap(p[i], p[j]);
+    out[i] = p[i];
+  }
+  return out;
+}
+
+void kmeans_update(const float* x, int64_t n, int d, int k, const int64_t* assign, float* cent) {
+  std::vector<double> sum((size_t)k * d, 0.0);
+  std::vector<int64_t> cnt(k, 0);
+  for (int64_t i = 0; i < n; i++) {
+    const int64_t c = assign[i];
+    cnt[c]++;
+    double* s = &sum[(size_t)c * d];
+    const float* xi = x + i * d;
+    for (int t = 0; t < d; t++) s[t] += (double)xi[t];
+  }
+  for (int c = 0; c < k; c++)
+    if (cnt[c] > 0)
+      for (int t = 0; t < d; t++) cent[(size_t)c * d + t] = (float)(sum[(size_t)c * d + t] / (double)cnt[c]);
+  const float eps = 1.0f / 1024.0f;
+  for (int c = 0; c < k; c++) {
+    if (cnt[c] != 0) continue;
+    int big = 0;
+    for (int j = 1; j < k; j++)
+      if (cnt[j] > cnt[big]) big = j;
+    for (int t = 0; t < d; t++) {
+      const float v = cent[(size_t)big * d + t];
+      if (t % 2 == 0) {
+        cent[(size_t)c * d + t] = v * (1.0f + eps);
+        cent[(size_t)big * d + t] = v * (1.0f - eps);
+      } else {
+        cent[(size_t)c * d + t] = v * (1.0f - eps);
+        cent[(size_t)big * d + t] = v * (1.0f + eps);
+      }
+    }
+    cnt[c] = cnt[big] / 2;
+    cnt[big] -= cnt[c];
+  }
+}
+
+constexpr size_t kChunkBytes = size_t(256) << 20;  // bound for [rows][cols] fp32 scratch
+
+}  // namespace
+
+struct ivfpq_index {
+  int d = 0, nlist = 0, M = 0, nbits = 8, ksub = 256, metric = IVFPQ_METRIC_L2, device = 0;
+  int nprobe = 1;
+  int list_lo = 0, list_hi = 0;
+  bool trained = false;
+  std::vector<float> centroids, codebook;
+  std::vector<std::vector<uint8_t>> lcodes;
+  std::vector<std::vector<int64_t>> lids;
+  int64_t ntotal = 0;
+  int64_t next_id = 0;
+
+  DevBuf d_cent, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off;
+  bool dirty = true;
+  hipStream_t stream = nullptr;
+  // scratch
+  DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
+  std::mutex mu;
+
+  // stage timing (HIP events recorded on the launch stream around each stage)
+  enum Stage { ST_COARSE = 0, ST_TABLES = 1, ST_SCAN = 2, ST_N = 3 };
+  bool timing = false;
+  struct Mark {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> ev_pool;
+
+  hipEvent_t take_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHECK(hipEventCreate(&e));
+    return e;
+  }
+  // returns an index into marks (or -1 when timing is off)
+  int mark_begin(int stage, hipStream_t s) {
+    if (!timing) return -1;
+    Mark m{stage, take_event(), take_event()};
+    HIPCHECK(hipEventRecord(m.a, s));
+    marks.push_back(m);
+    return (int)marks.size() - 1;
+  }
+  void mark_end(int idx, hipStream_t s) {
+    if (idx >= 0) HIPCHECK(hipEventRecord(marks[idx].b, s));
+  }
+  void collect_timing(double* ms, int64_t* cnt) {
+    for (int i = 0; i < ST_N; i++) {
+      ms[i] = 0.0;
+      cnt[i] = 0;
+    }
+    for (auto& m : marks) {
+      HIPCHECK(hipEventSynchronize(m.b));
+      float t = 0.f;
+      HIPCHECK(hipEventElapsedTime(&t, m.a, m.b));
+      ms[m.stage] += t;
+      cnt[m.stage] += 1;
+      ev_pool.push_back(m.a);
+      ev_pool.push_back(m.b);
+    }
+    marks.clear();
+  }
+
+  ~ivfpq_index() {
+    for (auto& m : marks) {
+      (void)hipEventDestroy(m.a);
+      (void)hipEventDestroy(m.b);
+    }
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  void init_stream() {
+    if (!stream) HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  }
+
+  // ---------------------------------------------------------------- helpers
+  // Row-wise top-1 of x [n][dd] against c (already on device with norms):
+  // writes assignments (host) for all rows. Uses w_x / w_xn / w_dist / w_D / w_I.
+  void assign_top1(const float* x_host, int64_t n, int dd, const float* dc, const float* dcn, int nc,
+                   int64_t* assign_host, const float* x_dev = nullptr) {
+    const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nc * 4)));
+    w_xn.ensure(sizeof(float) * rows);
+    w_dist.ensure(sizeof(float) * rows * nc);
+    w_D.ensure(sizeof(float) * rows);
+    w_I.ensure(sizeof(int64_t) * rows);
+    if (!x_dev) w_x.ensure(sizeof(float) * rows * dd);
+    for (int64_t r0 = 0; r0 < n; r0 += rows) {
+      const int64_t c = std::min(rows, n - r0);
+      const float* xd;
+      if (x_dev) {
+        xd = x_dev + r0 * dd;
+      } else {
+        HIPCHECK(hipMemcpyAsync(w_x.p, x_host + r0 * dd, sizeof(float) * c * dd, hipMemcpyHostToDevice, stream));
+        xd = w_x.as<float>();
+      }
+      launch_row_norms(xd, c, dd, w_xn.as<float>(), stream);
+      launch_l2_dist(xd, w_xn.as<float>(), c, dc, dcn, nc, dd, w_dist.as<float>(), stream);
+      launch_select_rows(w_dist.as<float>(), c, nc, 1, w_D.as<float>(), w_I.as<int64_t>(), stream);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(assign_host + r0, w_I.p, sizeof(int64_t) * c, hipMemcpyDeviceToHost, stream));
+      HIPCHECK(hipStreamSynchronize(stream));
+    }
+  }
+
+  void kmeans(const float* x, int64_t n, int dd, int k, int niter, uint64_t seed, float* cent) {
+    require(n >= k, "k-means: need at least as many training points as centroids (" + std::to_string(n) + " < " +
+                        std::to_string(k) + ")");
+    const auto init = rand_perm_prefix(n, k, seed);
+    for (int c = 0; c < k; c++) std::memcpy(cent + (size_t)c * dd, x + init[c] * dd, sizeof(float) * dd);
+    // keep the whole training set resident when it fits the scratch bound
+    DevBuf xall;
+    const bool resident = (size_t)n * dd * 4 <= (size_t(2) << 30);
+    if (resident) {
+      xall.ensure(sizeof(float) * n * dd);
+      HIPCHECK(hipMemcpyAsync(xall.p, x, sizeof(float) * n * dd, hipMemcpyHostToDevice, stream));
+    }
+    std::vector<int64_t> assign(n);
+    w_cent.ensure(sizeof(float) * k * dd);
+    w_cn.ensure(sizeof(float) * k);
+    for (int it = 0; it < niter; it++) {
+      HIPCHECK(hipMemcpyAsync(w_cent.p, cent, sizeof(float) * k * dd, hipMemcpyHostToDevice, stream));
+      launch_row_norms(w_cent.as<float>(), k, dd, w_cn.as<float>(), stream);
+      assign_top1(x, n, dd, w_cent.as<float>(), w_cn.as<float>(), k, assign.data(),
+                  resident ? xall.as<float>() : nullptr);
+      kmeans_update(x, n, dd, k, assign.data(), cent);
+    }
+  }
+
+  void upload_trained() {
+    d_cent.ensure(sizeof(float) * nlist * d);
+    d_cnorm.ensure(sizeof(float) * nlist);
+    d_cb.ensure(sizeof(float) * M * ksub * (d / M));
+    d_T1.ensure(sizeof(float) * (size_t)nlist * M * ksub);
+    HIPCHECK(hipMemcpyAsync(d_cent.p, centroids.data(), sizeof(float) * nlist * d, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipMemcpyAsync(d_cb.p, codebook.data(), sizeof(float) * codebook.size(), hipMemcpyHostToDevice,
+                            stream));
+    launch_row_norms(d_cent.as<float>(), nlist, d, d_cnorm.as<float>(), stream);
+    launch_precompute_T1(d_cent.as<float>(), nlist, d, d_cb.as<float>(), M, ksub, d_T1.as<float>(), stream);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(stream));
+    trained = true;
+  }
+
+  void upload_lists() {
+    if (!dirty) return;
+    std::vector<int64_t> off(nlist + 1, 0);
+    for (int l = 0; l < nlist; l++) off[l + 1] = off[l] + (int64_t)lids[l].size();
+    const int64_t tot = off[nlist];
+    std::vector<uint8_t> codes((size_t)tot * M);
+    std::vector<int64_t> ids((size_t)tot);
+    for (int l = 0; l < nlist; l++) {
+      if (!lids[l].empty()) {
+        std::memcpy(codes.data() + off[l] * M, lcodes[l].data(), lcodes[l].size());
+        std::memcpy(ids.data() + off[l], lids[l].data(), sizeof(int64_t) * lids[l].size());
+      }
+    }
+    d_codes.ensure(std::max<size_t>(16, codes.size()));
+    d_ids.ensure(std::max<size_t>(16, sizeof(int64_t) * ids.size()));
+    d_off.ensure(sizeof(int64_t) * off.size());
+    if (tot) {
+      HIPCHECK(hipMemcpyAsync(d_codes.p, codes.data(), codes.size(), hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipMemcpyAsync(d_ids.p, ids.data(), sizeof(int64_t) * ids.size(), hipMemcpyHostToDevice, stream));
+    }
+    HIPCHECK(hipMemcpyAsync(d_off.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    dirty = false;
+  }
+
+  void append(int64_t n, const int64_t* lno, const uint8_t* codes, const int64_t* ids) {
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t l = lno[i];
+      require(l >= 0 && l < nlist, "list number out of range");
+      if (l < list_lo || l >= list_hi) continue;  // another shard's list
+      lcodes[l].insert(lcodes[l].end(), codes + i * M, codes + (i + 1) * M);
+      lids[l].push_back(ids[i]);
+      ntotal++;
+    }
+    dirty = true;
+  }
+
+  int eff_nprobe() const { return std::min(nprobe, nlist); }
+
+  void check_search(int64_t n, int k) {
+    require(trained, "index is not trained");
+    require(n >= 0, "n must be >= 0");
+    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]");
+    require(metric == IVFPQ_METRIC_L2, "only METRIC_L2 is served on the GPU");
+  }
+
+  // The full search on device pointers, on stream s.  Iq/Dq non-null = preassigned.
+  void search_dev(int64_t n, const float* x, int k, float* D, int64_t* I, const int64_t* Iq, const float* Dq,
+                  bool preassigned, hipStream_t s) {
+    check_search(n, k);
+    upload_lists();
+    if (n == 0) return;
+    const int np = preassigned ? nprobe : eff_nprobe();
+    const size_t per_q = std::max<size_t>((size_t)nlist, (size_t)M * ksub) * 4;
+    const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / per_q));
+    w_T3.ensure(sizeof(float) * qc * M * ksub);
+    if (!preassigned) {
+      w_xn.ensure(sizeof(float) * qc);
+      w_dist.ensure(sizeof(float) * qc * nlist);
+      w_lists.ensure(sizeof(int64_t) * qc * np);
+      w_dis0.ensure(sizeof(float) * qc * np);
+    }
+    for (int64_t q0 = 0; q0 < n; q0 += qc) {
+      const int64_t c = std::min(qc, n - q0);
+      const float* xq = x + q0 * d;
+      const int64_t* lists;
+      const float* dis0;
+      if (preassigned) {
+        lists = Iq + q0 * np;
+        dis0 = Dq ? Dq + q0 * np : nullptr;
+      } else {
+        const int tm = mark_begin(ST_COARSE, s);
+        launch_row_norms(xq, c, d, w_xn.as<float>(), s);
+        launch_l2_dist(xq, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d,
+                       w_dist.as<float>(), s);
+        launch_select_rows(w_dist.as<float>(), c, nlist, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s);
+        mark_end(tm, s);
+        lists = w_lists.as<int64_t>();
+        dis0 = w_dis0.as<float>();
+      }
+      const int tt = mark_begin(ST_TABLES, s);
+      launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
+      mark_end(tt, s);
+      ScanArgs a;
+      a.T1 = d_T1.as<float>();
+      a.T3 = w_T3.as<float>();
+      a.codes = d_codes.as<uint8_t>();
+      a.ids = d_ids.as<int64_t>();
+      a.list_off = d_off.as<int64_t>();
+      a.probe_list = lists;
+      a.probe_dis0 = dis0;
+      a.nq = c;
+      a.nprobe = np;
+      a.k = k;
+      a.M = M;
+      a.list_lo = list_lo;
+      a.list_hi = list_hi;
+      a.outD = D + q0 * k;
+      a.outI = I + q0 * k;
+      const int ts = mark_begin(ST_SCAN, s);
+      launch_scan_topk(a, s);
+      mark_end(ts, s);
+      HIPCHECK(hipGetLastError());
+    }
+  }
+
+  void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {
+    require(trained, "index is not trained");
+    const int np = eff_nprobe();
+    const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
+    w_xn.ensure(sizeof(float) * qc);
+    w_dist.ensure(sizeof(float) * qc * nlist);
+    for (int64_t q0 = 0; q0 < n; q0 += qc) {
+      const int64_t c = std::min(qc, n - q0);
+      launch_row_norms(x + q0 * d, c, d, w_xn.as<float>(), s);
+      launch_l2_dist(x + q0 * d, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d,
+                     w_dist.as<float>(), s);
+      launch_select_rows(w_dist.as<float>(), c, nlist, np, Dq + q0 * np, Iq + q0 * np, s);
+      HIPCHECK(hipGetLastError());
+    }
+  }
+
+  // host-buffer search (copies in/out on the handle's stream)
+  void search_host(int64_t n, const float* x, int k, float* D, int64_t* I, const int64_t* Iq, const float* Dq,
+                   bool preassigned) {
+    check_search(n, k);
+    if (n == 0) return;
+    const int np = nprobe;
+    w_x.ensure(sizeof(float) * n * d);
+    DevBuf dD, dI, dIq, dDq;
+    dD.ensure(sizeof(float) * n * k);
+    dI.ensure(sizeof(int64_t) * n * k);
+    HIPCHECK(hipMemcpyAsync(w_x.p, x, sizeof(float) * n * d, hipMemcpyHostToDevice, stream));
+    if (preassigned) {
+      dIq.ensure(sizeof(int64_t) * n * np);
+      HIPCHECK(hipMemcpyAsync(dIq.p, Iq, sizeof(int64_t) * n * np, hipMemcpyHostToDevice, stream));
+      if (Dq) {
+        dDq.ensure(sizeof(float) * n * np);
+        HIPCHECK(hipMemcpyAsync(dDq.p, Dq, sizeof(float) * n * np, hipMemcpyHostToDevice, stream));
+      }
+    }
+    search_dev(n, w_x.as<float>(), k, dD.as<float>(), dI.as<int64_t>(), dIq.as<int64_t>(),
+               Dq ? dDq.as<float>() : nullptr, preassigned, stream);
+    HIPCHECK(hipMemcpyAsync(D, dD.p, sizeof(float) * n * k, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(I, dI.p, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+};
+
+// ====================================================================== C-ABI
+namespace {
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    g_err.clear();
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+  } catch (...) {
+    g_err = "unknown error";
+  }
+  return -1;
+}
+
+void check_handle(const ivfpq_index* h) { require(h != nullptr, "null index handle"); }
+
+}  // namespace
+
+extern "C" {
+
+const char* ivfpq_last_error(void) { return g_err.c_str(); }
+
+int ivfpq_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivfpq_index** out) {
+  return guarded([&] {
+    require(out != nullptr, "null output pointer");
+    require(d > 0 && nlist > 0 && M > 0, "d, nlist and M must be positive");
+    require(d % M == 0, "d must be a multiple of M");
+    require(nbits == 8, "only nbits=8 is supported");
+    require(scan_supported_M(M), "M=" + std::to_string(M) + " not supported on the GPU (8, 16, 32, 48, 64)");
+    require(metric == IVFPQ_METRIC_L2 || metric == IVFPQ_METRIC_INNER_PRODUCT, "unknown metric");
+    int ndev = 0;
+    HIPCHECK(hipGetDeviceCount(&ndev));
+    require(device >= 0 && device < ndev, "device ordinal out of range");
+    DeviceGuard g(device);
+    auto h = std::make_unique<ivfpq_index>();
+    h->d = d;
+    h->nlist = nlist;
+    h->M = M;
+    h->nbits = nbits;
+    h->ksub = 1 << nbits;
+    h->metric = metric;
+    h->device = device;
+    h->list_lo = 0;
+    h->list_hi = nlist;
+    h->lcodes.resize(nlist);
+    h->lids.resize(nlist);
+    h->init_stream();
+    *out = h.release();
+  });
+}
+
+int ivfpq_free(ivfpq_index* h) {
+  return guarded([&] {
+    if (!h) return;
+    DeviceGuard g(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    delete h;
+  });
+}
+
+int ivfpq_train(ivfpq_index* h, int64_t n, const float* x, int niter_coarse, int niter_pq, uint64_t seed) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(x != nullptr && n > 0, "empty training set");
+    const int d = h->d, M = h->M, dsub = d / M, ksub = h->ksub, nlist = h->nlist;
+    std::vector<float> cent((size_t)nlist * d);
+    h->kmeans(x, n, d, nlist, niter_coarse, seed, cent.data());
+    // residuals to the final coarse centroids
+    h->w_cent.ensure(sizeof(float) * nlist * d);
+    h->w_cn.ensure(sizeof(float) * nlist);
+    HIPCHECK(hipMemcpyAsync(h->w_cent.p, cent.data(), sizeof(float) * nlist * d, hipMemcpyHostToDevice, h->stream));
+    launch_row_norms(h->w_cent.as<float>(), nlist, d, h->w_cn.as<float>(), h->stream);
+    std::vector<int64_t> assign(n);
+    h->assign_top1(x, n, d, h->w_cent.as<float>(), h->w_cn.as<float>(), nlist, assign.data());
+    std::vector<float> sub((size_t)n * dsub);
+    std::vector<float> cb((size_t)M * ksub * dsub);
+    for (int m = 0; m < M; m++) {
+      for (int64_t i = 0; i < n; i++) {
+        const float* xi = x + i * d + m * dsub;
+        const float* ci = cent.data() + assign[i] * d + m * dsub;
+        for (int t = 0; t < dsub; t++) sub[(size_t)i * dsub + t] = xi[t] - ci[t];
+      }
+      h->kmeans(sub.data(), n, dsub, ksub, niter_pq, seed + 1 + (uint64_t)m, cb.data() + (size_t)m * ksub * dsub);
+    }
+    h->centroids = std::move(cent);
+    h->codebook = std::move(cb);
+    h->upload_trained();
+  });
+}
+
+int ivfpq_set_trained(ivfpq_index* h, const float* centroids, const float* codebook) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(centroids && codebook, "null centroids/codebook");
+    h->centroids.assign(centroids, centroids + (size_t)h->nlist * h->d);
+    h->codebook.assign(codebook, codebook + (size_t)h->M * h->ksub * (h->d / h->M));
+    h->upload_trained();
+  });
+}
+
+int ivfpq_add(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(h->trained, "index is not trained");
+    if (n <= 0) return;
+    require(x != nullptr, "null x");
+    const int d = h->d, M = h->M;
+    const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)h->nlist * 4)));
+    std::vector<int64_t> lno(rows);
+    std::vector<uint8_t> codes((size_t)rows * M);
+    std::vector<int64_t> seq;
+    h->w_x.ensure(sizeof(float) * rows * d);
+    h->w_xn.ensure(sizeof(float) * rows);
+    h->w_dist.ensure(sizeof(float) * rows * h->nlist);
+    h->w_D.ensure(sizeof(float) * rows);
+    h->w_lno.ensure(sizeof(int64_t) * rows);
+    h->w_codes.ensure((size_t)rows * M);
+    for (int64_t r0 = 0; r0 < n; r0 += rows) {
+      const int64_t c = std::min(rows, n - r0);
+      HIPCHECK(hipMemcpyAsync(h->w_x.p, x + r0 * d, sizeof(float) * c * d, hipMemcpyHostToDevice, h->stream));
+      launch_row_norms(h->w_x.as<float>(), c, d, h->w_xn.as<float>(), h->stream);
+      launch_l2_dist(h->w_x.as<float>(), h->w_xn.as<float>(), c, h->d_cent.as<float>(), h->d_cnorm.as<float>(),
+                     h->nlist, d, h->w_dist.as<float>(), h->stream);
+      launch_select_rows(h->w_dist.as<float>(), c, h->nlist, 1, h->w_D.as<float>(), h->w_lno.as<int64_t>(),
+                         h->stream);
+      launch_pq_encode(h->w_x.as<float>(), c, d, h->d_cent.as<float>(), h->w_lno.as<int64_t>(),
+                       h->d_cb.as<float>(), M, h->ksub, h->w_codes.as<uint8_t>(), h->stream);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(lno.data(), h->w_lno.p, sizeof(int64_t) * c, hipMemcpyDeviceToHost, h->stream));
+      HIPCHECK(hipMemcpyAsync(codes.data(), h->w_codes.p, (size_t)c * M, hipMemcpyDeviceToHost, h->stream));
+      HIPCHECK(hipStreamSynchronize(h->stream));
+      const int64_t* idp;
+      if (ids) {
+        idp = ids + r0;
+      } else {
+        seq.resize(c);
+        for (int64_t i = 0; i < c; i++) seq[i] = h->next_id + r0 + i;
+        idp = seq.data();
+      }
+      h->append(c, lno.data(), codes.data(), idp);
+    }
+    if (!ids) h->next_id += n;
+  });
+}
+
+int ivfpq_add_preencoded(ivfpq_index* h, int64_t n, const int64_t* list_no, const uint8_t* codes,
+                         const int64_t* ids) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (n <= 0) return;
+    require(list_no && codes, "null list_no/codes");
+    std::vector<int64_t> seq;
+    if (!ids) {
+      seq.resize(n);
+      for (int64_t i = 0; i < n; i++) seq[i] = h->next_id + i;
+      ids = seq.data();
+      h->next_id += n;
+    }
+    h->append(n, list_no, codes, ids);
+  });
+}
+
+int ivfpq_reset(ivfpq_index* h) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    for (auto& v : h->lcodes) v.clear();
+    for (auto& v : h->lids) v.clear();
+    h->ntotal = 0;
+    h->next_id = 0;
+    h->dirty = true;
+  });
+}
+
+int ivfpq_set_nprobe(ivfpq_index* h, int nprobe) {
+  return guarded([&] {
+    check_handle(h);
+    require(nprobe >= 1 && nprobe <= kMaxK, "nprobe must be in [1, " + std::to_string(kMaxK) + "]");
+    h->nprobe = nprobe;
+  });
+}
+
+int ivfpq_get_nprobe(const ivfpq_index* h) { return h ? h->nprobe : -1; }
+
+int ivfpq_set_list_range(ivfpq_index* h, int lo, int hi) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    require(0 <= lo && lo <= hi && hi <= h->nlist, "invalid list range");
+    require(h->ntotal == 0, "set the list range before adding vectors");
+    h->list_lo = lo;
+    h->list_hi = hi;
+  });
+}
+
+int ivfpq_search(ivfpq_index* h, int64_t n, const float* x, int k, float* D, int64_t* I) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(n == 0 || (x && D && I), "null buffer");
+    h->search_host(n, x, k, D, I, nullptr, nullptr, false);
+  });
+}
+
+int ivfpq_search_preassigned(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq, const float* Dq,
+                             float* D, int64_t* I) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(n == 0 || (x && Iq && D && I), "null buffer");
+    for (int64_t i = 0; i < n * h->nprobe; i++)
+      require(Iq[i] < h->nlist, "list id out of range in Iq");
+    h->search_host(n, x, k, D, I, Iq, Dq, true);
+  });
+}
+
+int ivfpq_search_device(ivfpq_index* h, int64_t n, const float* x, int k, float* D, int64_t* I, void* stream) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    h->search_dev(n, x, k, D, I, nullptr, nullptr, false, (hipStream_t)stream);
+  });
+}
+
+int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq,
+                                    const float* Dq, float* D, int64_t* I, void* stream) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    h->search_dev(n, x, k, D, I, Iq, Dq, true, (hipStream_t)stream);
+  });
+}
+
+int ivfpq_coarse_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, float* Dq, void* stream) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    h->coarse_dev(n, x, Iq, Dq, (hipStream_t)stream);
+  });
+}
+
+int ivfpq_merge_topk_device(int S, int64_t n, int k, const float* Din, const int64_t* Iin, float* Dout,
+                            int64_t* Iout, void* stream) {
+  return guarded([&] {
+    require(S >= 1 && k >= 1, "invalid merge shape");
+    launch_merge_topk(S, n, k, Din, Iin, Dout, Iout, (hipStream_t)stream);
+    HIPCHECK(hipGetLastError());
+  });
+}
+
+int ivfpq_set_timing(ivfpq_index* h, int on) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->timing = on != 0;
+  });
+}
+
+int ivfpq_get_timing(ivfpq_index* h, double* ms, int64_t* count) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(ms && count, "null output");
+    h->collect_timing(ms, count);
+  });
+}
+
+int64_t ivfpq_ntotal(const ivfpq_index* h) { return h ? h->ntotal : -1; }
+
+int ivfpq_is_trained(const ivfpq_index* h) { return h && h->trained ? 1 : 0; }
+
+int ivfpq_get_dims(const ivfpq_index* h, int* d, int* nlist, int* M, int* nbits, int* metric) {
+  return guarded([&] {
+    check_handle(h);
+    if (d) *d = h->d;
+    if (nlist) *nlist = h->nlist;
+    if (M) *M = h->M;
+    if (nbits) *nbits = h->nbits;
+    if (metric) *metric = h->metric;
+  });
+}
+
+int ivfpq_get_centroids(const ivfpq_index* h, float* out) {
+  return guarded([&] {
+    check_handle(h);
+    require(h->trained, "index is not trained");
+    std::memcpy(out, h->centroids.data(), sizeof(float) * h->centroids.size());
+  });
+}
+
+int ivfpq_get_codebook(const ivfpq_index* h, float* out) {
+  return guarded([&] {
+    check_handle(h);
+    require(h->trained, "index is not trained");
+    std::memcpy(out, h->codebook.data(), sizeof(float) * h->codebook.size());
+  });
+}
+
+int ivfpq_get_list_sizes(const ivfpq_index* h, int64_t* out) {
+  return guarded([&] {
+    check_handle(h);
+    for (int l = 0; l < h->nlist; l++) out[l] = (int64_t)h->lids[l].size();
+  });
+}
+
+int ivfpq_get_list(const ivfpq_index* h, int list, uint8_t* codes, int64_t* ids) {
+  return guarded([&] {
+    check_handle(h);
+    require(list >= 0 && list < h->nlist, "list id out of range");
+    if (codes) std::memcpy(codes, h->lcodes[list].data(), h->lcodes[list].size());
+    if (ids) std::memcpy(ids, h->lids[list].data(), sizeof(int64_t) * h->lids[list].size());
+  });
+}
+
+int ivfpq_get_precomputed_table(ivfpq_index* h, float* out) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(h->trained, "index is not trained");
+    HIPCHECK(hipMemcpy(out, h->d_T1.p, sizeof(float) * (size_t)h->nlist * h->M * h->ksub, hipMemcpyDeviceToHost));
+  });
+}
+
+// ----------------------------------------------------------------- save/load
+namespace {
+constexpr char kMagic[8] = {'C', 'H', 'I', 'V', 'F', 'P', 'Q', '1'};
+
+struct File {
+  FILE* f;
+  File(const char* p, const char* m) : f(std::fopen(p, m)) {
+    require(f != nullptr, std::string("cannot open ") + p);
+  }
+  ~File() {
+    if (f) std::fclose(f);
+  }
+  void w(const void* p, size_t n) { require(std::fwrite(p, 1, n, f) == n, "write failed"); }
+  void r(void* p, size_t n) { require(std::fread(p, 1, n, f) == n, "truncated index file"); }
+};
+}  // namespace
+
+int ivfpq_save(ivfpq_index* h, const char* path) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    File f(path, "wb");
+    f.w(kMagic, 8);
+    int32_t hdr[8] = {h->d, h->nlist, h->M, h->nbits, h->metric, h->nprobe, h->trained ? 1 : 0, 0};
+    f.w(hdr, sizeof(hdr));
+    int64_t cnt[2] = {h->ntotal, h->next_id};
+    f.w(cnt, sizeof(cnt));
+    if (h->trained) {
+      f.w(h->centroids.data(), sizeof(float) * h->centroids.size());
+      f.w(h->codebook.data(), sizeof(float) * h->codebook.size());
+    }
+    for (int l = 0; l < h->nlist; l++) {
+      int64_t sz = (int64_t)h->lids[l].size();
+      f.w(&sz, 8);
+      if (sz) {
+        f.w(h->lcodes[l].data(), h->lcodes[l].size());
+        f.w(h->lids[l].data(), sizeof(int64_t) * sz);
+      }
+    }
+  });
+}
+
+int ivfpq_load(const char* path, int device, ivfpq_index** out) {
+  ivfpq_index* h = nullptr;
+  int rc = guarded([&] {
+    File f(path, "rb");
+    char magic[8];
+    f.r(magic, 8);
+    require(std::memcmp(magic, kMagic, 8) == 0, "not a CHIVFPQ1 index file");
+    int32_t hdr[8];
+    f.r(hdr, sizeof(hdr));
+    int64_t cnt[2];
+    f.r(cnt, sizeof(cnt));
+    if (ivfpq_create(hdr[0], hdr[1], hdr[2], hdr[3], hdr[4], device, &h) != 0) throw std::runtime_error(g_err);
+    h->nprobe = hdr[5];
+    DeviceGuard g(device);
+    if (hdr[6]) {
+      h->centroids.resize((size_t)h->nlist * h->d);
+      h->codebook.resize((size_t)h->M * h->ksub * (h->d / h->M));
+      f.r(h->centroids.data(), sizeof(float) * h->centroids.size());
+      f.r(h->codebook.data(), sizeof(float) * h->codebook.size());
+      h->upload_trained();
+    }
+    for (int l = 0; l < h->nlist; l++) {
+      int64_t sz;
+      f.r(&sz, 8);
+      require(sz >= 0, "corrupt list size");
+      h->lcodes[l].resize((size_t)sz * h->M);
+      h->lids[l].resize((size_t)sz);
+      if (sz) {
+        f.r(h->lcodes[l].data(), h->lcodes[l].size());
+        f.r(h->lids[l].data(), sizeof(int64_t) * sz);
+      }
+    }
+    h->ntotal = cnt[0];
+    h->next_id = cnt[1];
+    h->dirty = true;
+    *out = h;
+  });
+  if (rc != 0 && h) {
+    std::string e = g_err;
+    ivfpq_free(h);
+    g_err = e;
+  }
+  return rc;
+}
+
+int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n, const float* x, int k, float* D,
+                      int64_t* I) {
+  return guarded([&] {
+    require(d > 0 && nb >= 0 && n >= 0, "invalid shape");
+    require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]");
+    if (n == 0) return;
+    DeviceGuard g(device);
+    hipStream_t s;
+    HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::unique_ptr<void, void (*)(void*)> sguard((void*)s, [](void* p) { (void)hipStreamDestroy((hipStream_t)p); });
+    DevBuf dxb, dbn, dx, dxn, ddist, dD, dI;
+    const int64_t nbb = std::max<int64_t>(nb, 1);
+    dxb.ensure(sizeof(float) * nbb * d);
+    dbn.ensure(sizeof(float) * nbb);
+    if (nb) HIPCHECK(hipMemcpyAsync(dxb.p, xb, sizeof(float) * nb * d, hipMemcpyHostToDevice, s));
+    launch_row_norms(dxb.as<float>(), nb, d, dbn.as<float>(), s);
+    const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nbb * 4)));
+    dx.ensure(sizeof(float) * qc * d);
+    dxn.ensure(sizeof(float) * qc);
+    ddist.ensure(sizeof(float) * qc * nbb);
+    dD.ensure(sizeof(float) * qc * k);
+    dI.ensure(sizeof(int64_t) * qc * k);
+    for (int64_t q0 = 0; q0 < n; q0 += qc) {
+      const int64_t c = std::min(qc, n - q0);
+      HIPCHECK(hipMemcpyAsync(dx.p, x + q0 * d, sizeof(float) * c * d, hipMemcpyHostToDevice, s));
+      launch_row_norms(dx.as<float>(), c, d, dxn.as<float>(), s);
+      launch_l2_dist(dx.as<float>(), dxn.as<float>(), c, dxb.as<float>(), dbn.as<float>(), (int)nb, d,
+                     ddist.as<float>(), s);
+      launch_select_rows(ddist.as<float>(), c, (int)nb, k, dD.as<float>(), dI.as<int64_t>(), s);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipMemcpyAsync(D + q0 * k, dD.p, sizeof(float) * c * k, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipMemcpyAsync(I + q0 * k, dI.p, sizeof(int64_t) * c * k, hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+    }
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,494 @@
+"""Faiss-compatible index classes backed by the gfx950 engine (libivfpq.so).
+
+The surface mirrors what Chameleon's callers use on ``faiss`` (SURVEY.md
+§8(b)):
+
+* ``IndexIVFPQ(quantizer, d, nlist, M, nbits)`` with ``train / add /
+  add_with_ids / search / search_preassigned / reset``, ``nprobe``,
+  ``ntotal``, ``d``, ``is_trained``, ``quantizer``, ``pq.centroids``,
+  ``invlists.{list_size,get_ids,get_codes,imbalance_factor}``,
+  ``precomputed_table``, ``parallel_mode``
+  (``bench_polysemous_1bn.py:272-291, 343-345, 368, 422, 430``;
+  ``beir/beir/retrieval/search/dense/faiss_index.py:13-96``;
+  ``ralm/retriever/faiss_retriever.py:18-275``;
+  ``my_faiss_extract_scripts/extract_FPGA_required_data.py:174-248``);
+* ``IndexFlatL2`` (the coarse quantizer; exact search on the GPU);
+* ``index_factory``, ``ParameterSpace``, ``read_index / write_index``,
+  ``swig_ptr``, ``vector_to_array``, ``get_num_gpus``.
+
+Numpy conventions as Faiss: float32 C-contiguous in; ``D`` float32 and ``I``
+int64 out; missing results are (FLT_MAX, -1).  Errors raise ``RuntimeError``
+(Faiss's SWIG layer turns ``FaissException`` into ``RuntimeError`` too).
+"""
+from __future__ import annotations
+
+import ctypes
+import re
+
+import numpy as np
+
+from . import _lib
+
+METRIC_INNER_PRODUCT = 0
+METRIC_L2 = 1
+MAX_K = 1024
+
+
+def _f32(x, d=None, name="x"):
+    a = np.ascontiguousarray(x, dtype=np.float32)
+    if a.ndim != 2 or (d is not None and a.shape[1] != d):
+        raise RuntimeError(f"{name} must be a float32 matrix with {d} columns, got shape {a.shape}")
+    return a
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t)
+
+
+def swig_ptr(a):
+    """Faiss passes raw pointers to the 8-argument search_preassigned; here the
+    array itself is passed through (faiss_retriever.py:217-223)."""
+    return a
+
+
+def vector_to_array(v):
+    return np.asarray(v).copy()
+
+
+def get_num_gpus():
+    return int(_lib.load().ivfpq_device_count())
+
+
+def _default_device():
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            return torch.cuda.current_device()
+    except Exception:
+        pass
+    return 0
+
+
+class IndexFlatL2:
+    """Exact L2 search (faiss.IndexFlatL2).  As an IVF quantizer it holds the
+    coarse centroids (``quantizer.xb``, extract_FPGA_required_data.py:174-184);
+    standalone, ``search`` runs the GPU distance + select kernels (the
+    IndexScanner coarse service, ralm/index_scanner/index_scanner.py:61-77)."""
+
+    metric_type = METRIC_L2
+    is_trained = True
+
+    def __init__(self, d, device=None):
+        self.d = d
+        self.device = _default_device() if device is None else device
+        self._xb = np.zeros((0, d), np.float32)
+
+    @property
+    def ntotal(self):
+        return self._xb.shape[0]
+
+    @property
+    def xb(self):
+        return self._xb.reshape(-1)
+
+    def add(self, x):
+        x = _f32(x, self.d)
+        self._xb = np.concatenate([self._xb, x]) if self.ntotal else x.copy()
+
+    def reset(self):
+        self._xb = np.zeros((0, self.d), np.float32)
+
+    def reconstruct(self, i):
+        return self._xb[i].copy()
+
+    def reconstruct_n(self, i0, n):
+        return self._xb[i0:i0 + n].copy()
+
+    def train(self, x):
+        pass
+
+    def search(self, x, k):
+        x = _f32(x, self.d)
+        n = x.shape[0]
+        if not 1 <= k <= MAX_K:
+            raise RuntimeError(f"k must be in [1, {MAX_K}]")
+        D = np.empty((n, k), np.float32)
+        I = np.empty((n, k), np.int64)
+        L = _lib.load()
+        _lib.check(L.ivfpq_flat_search(self.device, self.d, self.ntotal, _ptr(self._xb, _lib.c_f32p), n,
+                                       _ptr(x, _lib.c_f32p), k, _ptr(D, _lib.c_f32p), _ptr(I, _lib.c_i64p)))
+        return D, I
+
+
+class _ProductQuantizer:
+    """index.pq view: M, nbits, ksub, dsub and ``centroids`` (M*256*dsub floats,
+    the layout of faiss pq.centroids)."""
+
+    def __init__(self, owner):
+        self._o = owner
+
+    M = property(lambda self: self._o.M)
+    nbits = property(lambda self: self._o.nbits)
+    ksub = property(lambda self: 1 << self._o.nbits)
+    dsub = property(lambda self: self._o.d // self._o.M)
+    code_size = property(lambda self: self._o.M * self._o.nbits // 8)
+
+    @property
+    def centroids(self):
+        return self._o.codebook().reshape(-1)
+
+    def get_centroids(self, m, j):
+        return self._o.codebook()[m, j].copy()
+
+
+class _InvertedLists:
+    """index.invlists view (faiss ArrayInvertedLists read API)."""
+
+    def __init__(self, owner):
+        self._o = owner
+
+    @property
+    def nlist(self):
+        return self._o.nlist
+
+    @property
+    def code_size(self):
+        return self._o.M
+
+    def list_sizes(self):
+        out = np.empty(self._o.nlist, np.int64)
+        _lib.check(_lib.load().ivfpq_get_list_sizes(self._o._h, _ptr(out, _lib.c_i64p)))
+        return out
+
+    def list_size(self, l):
+        return int(self.list_sizes()[l])
+
+    def _get(self, l):
+        n = self.list_size(l)
+        codes = np.empty((n, self._o.M), np.uint8)
+        ids = np.empty(n, np.int64)
+        _lib.check(_lib.load().ivfpq_get_list(self._o._h, int(l), _ptr(codes, _lib.c_u8p),
+                                              _ptr(ids, _lib.c_i64p)))
+        return codes, ids
+
+    def get_codes(self, l):
+        return self._get(l)[0].reshape(-1)
+
+    def get_ids(self, l):
+        return self._get(l)[1]
+
+    def imbalance_factor(self):
+        """faiss InvertedLists::imbalance_factor: nlist * sum(n_l^2) / ntotal^2."""
+        s = self.list_sizes().astype(np.float64)
+        tot = s.sum()
+        return float(len(s) * (s * s).sum() / (tot * tot)) if tot else 0.0
+
+
+class IndexIVFPQ:
+    """faiss.IndexIVFPQ (L2, by_residual, precomputed tables) on one MI355X."""
+
+    by_residual = True
+    use_precomputed_table = 1
+    polysemous_ht = 0
+
+    def __init__(self, quantizer, d, nlist, M, nbits=8, metric=METRIC_L2, device=None, _handle=None):
+        self.d = int(d)
+        self.nlist = int(nlist)
+        self.M = int(M)
+        self.nbits = int(nbits)
+        self.metric_type = metric
+        self.device = _default_device() if device is None else int(device)
+        self.quantizer = quantizer if quantizer is not None else IndexFlatL2(d, self.device)
+        self.parallel_mode = 0  # accepted for faiss_retriever.py:71; queries are always independent
+        self.verbose = False
+        self.niter_coarse = 25
+        self.niter_pq = 25
+        self.seed = 1234
+        L = _lib.load()
+        if _handle is not None:
+            self._h = _handle
+        else:
+            h = _lib.c_handle()
+            _lib.check(L.ivfpq_create(self.d, self.nlist, self.M, self.nbits, metric, self.device, ctypes.byref(h)))
+            self._h = h
+        self.pq = _ProductQuantizer(self)
+        self.invlists = _InvertedLists(self)
+        self._codebook_cache = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib._lib.ivfpq_free(h)
+            self._h = None
+
+    # ------------------------------------------------------------ properties
+    @property
+    def ntotal(self):
+        return int(_lib.load().ivfpq_ntotal(self._h))
+
+    @property
+    def is_trained(self):
+        return bool(_lib.load().ivfpq_is_trained(self._h))
+
+    @property
+    def nprobe(self):
+        return int(_lib.load().ivfpq_get_nprobe(self._h))
+
+    @nprobe.setter
+    def nprobe(self, p):
+        _lib.check(_lib.load().ivfpq_set_nprobe(self._h, int(p)))
+
+    @property
+    def code_size(self):
+        return self.M
+
+    def codebook(self):
+        if self._codebook_cache is None:
+            cb = np.empty((self.M, 1 << self.nbits, self.d // self.M), np.float32)
+            _lib.check(_lib.load().ivfpq_get_codebook(self._h, _ptr(cb, _lib.c_f32p)))
+            self._codebook_cache = cb
+        return self._codebook_cache
+
+    def centroids(self):
+        c = np.empty((self.nlist, self.d), np.float32)
+        _lib.check(_lib.load().ivfpq_get_centroids(self._h, _ptr(c, _lib.c_f32p)))
+        return c
+
+    @property
+    def precomputed_table(self):
+        t = np.empty((self.nlist, self.M, 1 << self.nbits), np.float32)
+        _lib.check(_lib.load().ivfpq_get_precomputed_table(self._h, _ptr(t, _lib.c_f32p)))
+        return t.reshape(-1)
+
+    def _sync_quantizer(self):
+        if isinstance(self.quantizer, IndexFlatL2):
+            self.quantizer.reset()
+            self.quantizer.add(self.centroids())
+
+    # ----------------------------------------------------------- build path
+    def train(self, x):
+        x = _f32(x, self.d)
+        _lib.check(_lib.load().ivfpq_train(self._h, x.shape[0], _ptr(x, _lib.c_f32p), self.niter_coarse,
+                                           self.niter_pq, self.seed))
+        self._codebook_cache = None
+        self._sync_quantizer()
+
+    def set_trained(self, centroids, codebook):
+        """Install trained quantizers (coarse centroids [nlist][d], PQ codebook [M][256][d/M])."""
+        c = _f32(np.asarray(centroids).reshape(self.nlist, self.d), self.d, "centroids")
+        cb = np.ascontiguousarray(codebook, np.float32).reshape(-1)
+        if cb.size != self.M * (1 << self.nbits) * (self.d // self.M):
+            raise RuntimeError("codebook has the wrong size")
+        _lib.check(_lib.load().ivfpq_set_trained(self._h, _ptr(c, _lib.c_f32p), _ptr(cb, _lib.c_f32p)))
+        self._codebook_cache = None
+        self._sync_quantizer()
+
+    def add(self, x):
+        x = _f32(x, self.d)
+        _lib.check(_lib.load().ivfpq_add(self._h, x.shape[0], _ptr(x, _lib.c_f32p), None))
+
+    def add_with_ids(self, x, ids):
+        x = _f32(x, self.d)
+        ids = np.ascontiguousarray(ids, np.int64).reshape(-1)
+        if ids.shape[0] != x.shape[0]:
+            raise RuntimeError("ids and x have different lengths")
+        _lib.check(_lib.load().ivfpq_add(self._h, x.shape[0], _ptr(x, _lib.c_f32p), _ptr(ids, _lib.c_i64p)))
+
+    def add_preencoded(self, list_no, codes, ids=None):
+        list_no = np.ascontiguousarray(list_no, np.int64).reshape(-1)
+        codes = np.ascontiguousarray(codes, np.uint8).reshape(-1, self.M)
+        n = list_no.shape[0]
+        if codes.shape[0] != n:
+            raise RuntimeError("codes and list_no have different lengths")
+        idp = None
+        if ids is not None:
+            ids = np.ascontiguousarray(ids, np.int64).reshape(-1)
+            idp = _ptr(ids, _lib.c_i64p)
+        _lib.check(_lib.load().ivfpq_add_preencoded(self._h, n, _ptr(list_no, _lib.c_i64p),
+                                                    _ptr(codes, _lib.c_u8p), idp))
+
+    def reset(self):
+        _lib.check(_lib.load().ivfpq_reset(self._h))
+
+    def set_list_range(self, lo, hi):
+        """Keep and scan only inverted lists [lo, hi) (list-range sharding)."""
+        _lib.check(_lib.load().ivfpq_set_list_range(self._h, int(lo), int(hi)))
+
+    # ------------------------------------------------------------ search path
+    def _check_k(self, k):
+        if not 1 <= int(k) <= MAX_K:
+            raise RuntimeError(f"k must be in [1, {MAX_K}], got {k}")
+
+    def search(self, x, k):
+        x = _f32(x, self.d)
+        self._check_k(k)
+        n = x.shape[0]
+        D = np.empty((n, k), np.float32)
+        I = np.empty((n, k), np.int64)
+        _lib.check(_lib.load().ivfpq_search(self._h, n, _ptr(x, _lib.c_f32p), int(k), _ptr(D, _lib.c_f32p),
+                                            _ptr(I, _lib.c_i64p)))
+        return D, I
+
+    def search_preassigned(self, *args):
+        """Either ``search_preassigned(x, k, Iq, Dq=None) -> (D, I)`` or the
+        Faiss C++ form ``search_preassigned(n, x, k, Iq, Dq, D, I, store_pairs)``
+        that fills D and I (faiss_retriever.py:217-223)."""
+        if len(args) >= 7:
+            n, x, k, Iq, Dq, D, I = args[:7]
+            if len(args) > 7 and args[7]:
+                raise RuntimeError("store_pairs is not supported")
+            Dr, Ir = self._search_preassigned(x, k, Iq, Dq)
+            np.copyto(np.asarray(D).reshape(Dr.shape), Dr)
+            np.copyto(np.asarray(I).reshape(Ir.shape), Ir)
+            return None
+        x, k, Iq = args[:3]
+        Dq = args[3] if len(args) > 3 else None
+        return self._search_preassigned(x, k, Iq, Dq)
+
+    def _search_preassigned(self, x, k, Iq, Dq=None):
+        x = _f32(np.asarray(x).reshape(-1, self.d), self.d)
+        self._check_k(k)
+        n = x.shape[0]
+        Iq = np.ascontiguousarray(Iq, np.int64).reshape(n, -1)
+        if Iq.shape[1] != self.nprobe:
+            raise RuntimeError(f"Iq must have nprobe={self.nprobe} columns, got {Iq.shape[1]}")
+        Dqp = None
+        if Dq is not None:
+            Dq = np.ascontiguousarray(Dq, np.float32).reshape(Iq.shape)
+            Dqp = _ptr(Dq, _lib.c_f32p)
+        D = np.empty((n, k), np.float32)
+        I = np.empty((n, k), np.int64)
+        _lib.check(_lib.load().ivfpq_search_preassigned(self._h, n, _ptr(x, _lib.c_f32p), int(k),
+                                                        _ptr(Iq, _lib.c_i64p), Dqp, _ptr(D, _lib.c_f32p),
+                                                        _ptr(I, _lib.c_i64p)))
+        return D, I
+
+    # ------------------------------------------------------------ stage timing
+    STAGES = ("coarse", "tables", "scan")
+
+    def set_timing(self, on=True):
+        _lib.check(_lib.load().ivfpq_set_timing(self._h, 1 if on else 0))
+
+    def get_timing(self):
+        """{stage: (total_ms, launches)} since the last call (waits for the events)."""
+        ms = (ctypes.c_double * 3)()
+        cnt = (ctypes.c_int64 * 3)()
+        _lib.check(_lib.load().ivfpq_get_timing(self._h, ms, cnt))
+        return {s: (ms[i], cnt[i]) for i, s in enumerate(self.STAGES)}
+
+    # ------------------------------------------------- device (torch) entry points
+    def search_device(self, x, k, D=None, I=None, stream=None):
+        """Search with inputs resident in HBM.  ``x`` is a torch float32 CUDA
+        tensor [n, d]; returns torch (D, I) on the same device, launched on
+        ``stream`` (default: torch's current stream)."""
+        import torch
+
+        n = x.shape[0]
+        self._check_k(k)
+        if D is None:
+            D = torch.empty((n, k), dtype=torch.float32, device=x.device)
+        if I is None:
+            I = torch.empty((n, k), dtype=torch.int64, device=x.device)
+        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(_lib.load().ivfpq_search_device(self._h, n, x.data_ptr(), int(k), D.data_ptr(), I.data_ptr(),
+                                                   ctypes.c_void_p(s)))
+        return D, I
+
+    def search_preassigned_device(self, x, k, Iq, Dq=None, D=None, I=None, stream=None):
+        import torch
+
+        n = x.shape[0]
+        self._check_k(k)
+        if D is None:
+            D = torch.empty((n, k), dtype=torch.float32, device=x.device)
+        if I is None:
+            I = torch.empty((n, k), dtype=torch.int64, device=x.device)
+        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(_lib.load().ivfpq_search_preassigned_device(
+            self._h, n, x.data_ptr(), int(k), Iq.data_ptr(), Dq.data_ptr() if Dq is not None else None,
+            D.data_ptr(), I.data_ptr(), ctypes.c_void_p(s)))
+        return D, I
+
+    def coarse_device(self, x, Iq=None, Dq=None, stream=None):
+        import torch
+
+        n = x.shape[0]
+        p = min(self.nprobe, self.nlist)
+        if Iq is None:
+            Iq = torch.empty((n, p), dtype=torch.int64, device=x.device)
+        if Dq is None:
+            Dq = torch.empty((n, p), dtype=torch.float32, device=x.device)
+        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        _lib.check(_lib.load().ivfpq_coarse_device(self._h, n, x.data_ptr(), Iq.data_ptr(), Dq.data_ptr(),
+                                                   ctypes.c_void_p(s)))
+        return Dq, Iq
+
+
+def merge_topk_device(Ds, Is, stream=None):
+    """Merge S sorted partial results (torch [S, n, k]) into [n, k] on the GPU."""
+    import torch
+
+    S, n, k = Ds.shape
+    D = torch.empty((n, k), dtype=torch.float32, device=Ds.device)
+    I = torch.empty((n, k), dtype=torch.int64, device=Ds.device)
+    s = stream if stream is not None else torch.cuda.current_stream(Ds.device).cuda_stream
+    _lib.check(_lib.load().ivfpq_merge_topk_device(S, n, k, Ds.data_ptr(), Is.data_ptr(), D.data_ptr(),
+                                                   I.data_ptr(), ctypes.c_void_p(s)))
+    return D, I
+
+
+# ------------------------------------------------------------------ factory / IO
+
+_FACTORY_RE = re.compile(r"^IVF(\d+),PQ(\d+)(?:x(\d+))?$")
+
+
+def parse_factory(key):
+    m = _FACTORY_RE.match(key.replace(" ", ""))
+    if not m:
+        raise RuntimeError(f"index_factory: unsupported key {key!r} (supported: 'IVF<nlist>,PQ<M>[x8]')")
+    nbits = int(m.group(3)) if m.group(3) else 8
+    return int(m.group(1)), int(m.group(2)), nbits
+
+
+def index_factory(d, key, metric=METRIC_L2, device=None):
+    """faiss.index_factory(d, "IVF1024,PQ16") (bench_polysemous_1bn.py:272)."""
+    nlist, M, nbits = parse_factory(key)
+    return IndexIVFPQ(IndexFlatL2(d, device), d, nlist, M, nbits, metric, device)
+
+
+class ParameterSpace:
+    """faiss.ParameterSpace subset: set_index_parameters(index, "nprobe=16")."""
+
+    def initialize(self, index):
+        pass
+
+    def set_index_parameter(self, index, name, value):
+        if name != "nprobe":
+            raise RuntimeError(f"unsupported parameter {name}")
+        index.nprobe = int(value)
+
+    def set_index_parameters(self, index, params):
+        for kv in params.split(","):
+            if not kv:
+                continue
+            name, value = kv.split("=")
+            self.set_index_parameter(index, name.strip(), float(value))
+
+
+def write_index(index, path):
+    _lib.check(_lib.load().ivfpq_save(index._h, str(path).encode()))
+
+
+def read_index(path, device=None):
+    device = _default_device() if device is None else device
+    h = _lib.c_handle()
+    L = _lib.load()
+    _lib.check(L.ivfpq_load(str(path).encode(), device, ctypes.byref(h)))
+    dims = [ctypes.c_int() for _ in range(5)]
+    _lib.check(L.ivfpq_get_dims(h, *[ctypes.byref(v) for v in dims]))
+    d, nlist, M, nbits, metric = [v.value for v in dims]
+    idx = IndexIVFPQ(None, d, nlist, M, nbits, metric, device, _handle=h)
+    if idx.is_trained:
+        idx._sync_quantizer()
+    return idx

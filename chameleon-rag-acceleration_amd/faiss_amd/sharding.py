@@ -1,0 +1,119 @@
+"""Multi-GPU IVF-PQ: inverted-list-range sharding with an RCCL exchange.
+
+Replaces Faiss ``IndexShards`` (``bench_gpu_1bn.py:605-616``: query broadcast
+to every GPU, per-shard top-k, host-side merge by CPU threads) and the host
+``np.argsort`` shard merge (``bench_multi_cpu_performance_OSDI.py:203-218``).
+
+One process per GPU (``torch.distributed``, backend ``nccl`` = RCCL on ROCm):
+
+* GPU ``r`` stores and scans only the inverted lists ``[lo_r, hi_r)``; the
+  ranges are contiguous and balanced by code bytes (lists are imbalanced,
+  ``bench_polysemous_1bn.py:368``).
+* Every rank holds the global query batch (``world`` slices of ``B`` queries,
+  slice ``j`` owned by rank ``j``), computes the coarse probe for it, scans its
+  own lists and produces a partial sorted top-k per query.
+* One ``all_to_all`` sends slice ``j`` of every partial result to rank ``j``
+  (``world * B * k * 12`` bytes per rank — latency-bound on xGMI), and each
+  rank merges its ``world`` partial lists by (distance, label) on the GPU.
+
+The exchange is written against plain ``torch.distributed`` so it runs under
+``gloo`` on CPU tensors for the multi-process tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def balanced_list_ranges(list_sizes, world, code_size=1):
+    """Contiguous list ranges [(lo, hi)] * world with near-equal code bytes.
+
+    Greedy prefix cut: range r ends at the first list where the cumulative
+    bytes reach (r + 1) / world of the total.  Every range is non-empty when
+    nlist >= world.
+    """
+    sizes = np.asarray(list_sizes, dtype=np.int64) * int(code_size)
+    nlist = sizes.shape[0]
+    if world < 1 or world > nlist:
+        raise ValueError("need 1 <= world <= nlist")
+    csum = np.cumsum(sizes)
+    total = csum[-1] if nlist else 0
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        cut = int(np.searchsorted(csum, target, side="left")) + 1
+        cut = max(cut, bounds[-1] + 1)  # non-empty
+        cut = min(cut, nlist - (world - r))  # leave one list per remaining rank
+        bounds.append(cut)
+    bounds.append(nlist)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def exchange_partials(Dp, Ip, world, group=None):
+    """all_to_all of per-rank partial results.
+
+    Dp, Ip: [world * B, k] partial top-k over this rank's lists for the global
+    batch.  Returns (Ds, Is) of shape [world, B, k]: entry s holds rank s's
+    partial for this rank's query slice.
+    """
+    import torch
+    import torch.distributed as dist
+
+    n, k = Dp.shape
+    B = n // world
+    Ds = torch.empty((world, B, k), dtype=Dp.dtype, device=Dp.device)
+    Is = torch.empty((world, B, k), dtype=Ip.dtype, device=Ip.device)
+    if world == 1:
+        Ds[0].copy_(Dp)
+        Is[0].copy_(Ip)
+        return Ds, Is
+    if dist.get_backend(group) == "gloo":  # gloo has no all_to_all: gather then slice
+        rank = dist.get_rank(group)
+        gD = [torch.empty_like(Dp) for _ in range(world)]
+        gI = [torch.empty_like(Ip) for _ in range(world)]
+        dist.all_gather(gD, Dp.contiguous(), group=group)
+        dist.all_gather(gI, Ip.contiguous(), group=group)
+        for s in range(world):
+            Ds[s].copy_(gD[s][rank * B:(rank + 1) * B])
+            Is[s].copy_(gI[s][rank * B:(rank + 1) * B])
+        return Ds, Is
+    dist.all_to_all_single(Ds.view(world * B, k), Dp.contiguous(), group=group)
+    dist.all_to_all_single(Is.view(world * B, k), Ip.contiguous(), group=group)
+    return Ds, Is
+
+
+def merge_partials_reference(Ds, Is):
+    """Host merge of [S, n, k] sorted partials by (distance, label); -1 labels last.
+    Test reference for the device merge (faiss_amd.merge_topk_device)."""
+    Ds = np.asarray(Ds)
+    Is = np.asarray(Is)
+    S, n, k = Ds.shape
+    D = np.empty((n, k), np.float32)
+    I = np.empty((n, k), np.int64)
+    big = np.iinfo(np.int64).max
+    for q in range(n):
+        dd = Ds[:, q].reshape(-1)
+        ii = Is[:, q].reshape(-1)
+        o = np.lexsort((np.where(ii < 0, big, ii), dd))[:k]
+        D[q] = dd[o]
+        I[q] = ii[o]
+    return D, I
+
+
+class ShardedSearch:
+    """Per-rank driver of a list-range-sharded search.
+
+    ``local_search(xq_global, k) -> (Dp, Ip)`` runs this rank's shard (the GPU
+    engine in production); ``merge(Ds, Is) -> (D, I)`` merges the exchanged
+    partials (``faiss_amd.merge_topk_device`` in production).
+    """
+
+    def __init__(self, local_search, merge, world, group=None):
+        self.local_search = local_search
+        self.merge = merge
+        self.world = world
+        self.group = group
+
+    def search(self, xq_global, k):
+        Dp, Ip = self.local_search(xq_global, k)
+        Ds, Is = exchange_partials(Dp, Ip, self.world, self.group)
+        return self.merge(Ds, Is)

@@ -1,0 +1,129 @@
+/*
+ * ivfpq.h — C-ABI of libivfpq.so, the MI355X (gfx950) IVF-PQ engine.
+ *
+ * Drop-in boundary for the IVF-PQ search path that Chameleon reaches through
+ * Faiss's Python surface.  Each entry point names the
+ * Faiss / Chameleon interface it replaces.  Plain pointers and sizes only;
+ * host entry points take host buffers (numpy), *_device entry points take
+ * device pointers plus a hipStream_t passed as void*.
+ *
+ * Conventions (as faiss.IndexIVFPQ):
+ *   x: float32 [n][d] row-major;  D: float32 [n][k] ascending L2;
+ *   I: int64 [n][k] labels, -1 (with distance FLT_MAX) where fewer than k
+ *   results exist.  Ties are ordered by (distance, label).
+ * Errors: every int-returning function returns 0 on success and -1 on error;
+ * ivfpq_last_error() gives the thread-local message (the Python layer raises
+ * RuntimeError, as Faiss's SWIG wrapper does for FaissException).
+ * Thread-safety: one mutex per handle; train/add/search serialize on it.
+ */
+#ifndef CHAMELEON_IVFPQ_H
+#define CHAMELEON_IVFPQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ivfpq_index ivfpq_index;
+
+#define IVFPQ_METRIC_INNER_PRODUCT 0 /* faiss.METRIC_INNER_PRODUCT (not yet served on GPU) */
+#define IVFPQ_METRIC_L2 1            /* faiss.METRIC_L2 */
+
+/* Last error message of the calling thread ("" if none). */
+const char* ivfpq_last_error(void);
+
+/* Number of visible HIP devices (faiss.get_num_gpus, beir faiss_index.py:46). */
+int ivfpq_device_count(void);
+
+/* faiss.IndexIVFPQ(quantizer, d, nlist, M, nbits) / index_factory(d, "IVF<nlist>,PQ<M>")
+ * (IVFPQ_random_dataset.py:22-24, bench_polysemous_1bn.py:272).  nbits must be 8. */
+int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivfpq_index** out);
+int ivfpq_free(ivfpq_index* h);
+
+/* Index.train(x)  (bench_polysemous_1bn.py:283; beir faiss_index.py FaissTrainIndex.build).
+ * Lloyd k-means on the GPU: coarse (niter_coarse) then one per sub-space (niter_pq). */
+int ivfpq_train(ivfpq_index* h, int64_t n, const float* x, int niter_coarse, int niter_pq, uint64_t seed);
+
+/* Index.add(x) / add_with_ids(x, ids)  (bench_polysemous_1bn.py:343-345; beir faiss_index.py:41-42).
+ * ids == NULL assigns ntotal, ntotal+1, ...  Encoding runs on the GPU. */
+int ivfpq_add(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids);
+
+/* invlists.add_entries with precomputed (list, code, id) triples, e.g. from a
+ * loaded Faiss index or another shard.  codes: uint8 [n][M]. */
+int ivfpq_add_preencoded(ivfpq_index* h, int64_t n, const int64_t* list_no, const uint8_t* codes,
+                         const int64_t* ids);
+
+/* Index.reset(): drop all inverted-list entries, keep the trained quantizers. */
+int ivfpq_reset(ivfpq_index* h);
+
+/* index.nprobe = p / ParameterSpace().set_index_parameters(index, "nprobe=p")
+ * (faiss_retriever.py:170-176, bench_polysemous_1bn.py:422).  Clamped to nlist at search. */
+int ivfpq_set_nprobe(ivfpq_index* h, int nprobe);
+int ivfpq_get_nprobe(const ivfpq_index* h);
+
+/* Shard range: only inverted lists in [lo, hi) are stored and scanned (list-range sharding,
+ * SURVEY.md §8(e); replaces IndexShards, bench_gpu_1bn.py:605-616).  Default [0, nlist). */
+int ivfpq_set_list_range(ivfpq_index* h, int lo, int hi);
+
+/* Index.search(x, k) -> (D, I)  (beir faiss_index.py:22, bench_polysemous_1bn.py:430,
+ * faiss_retriever.py:254, faiss_server.py:197).  Host buffers. k <= 1024. */
+int ivfpq_search(ivfpq_index* h, int64_t n, const float* x, int k, float* D, int64_t* I);
+
+/* IndexIVF::search_preassigned(n, x, k, Iq, Dq, D, I, store_pairs=False)
+ * (faiss_retriever.py:217-223) and faiss.contrib.ivf_tools.search_preassigned
+ * (faiss_retriever.py:265).  Iq: int64 [n][nprobe] list ids (-1 = skip);
+ * Dq: float32 [n][nprobe] coarse distances, NULL = zeros (the upstream default). */
+int ivfpq_search_preassigned(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq, const float* Dq,
+                             float* D, int64_t* I);
+
+/* Device-pointer variants (inputs already resident in HBM; stream = hipStream_t, NULL = default).
+ * The whole search: coarse probe, T3, fused LUT + scan + top-k. */
+int ivfpq_search_device(ivfpq_index* h, int64_t n, const float* x, int k, float* D, int64_t* I, void* stream);
+int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq,
+                                    const float* Dq, float* D, int64_t* I, void* stream);
+/* Stage entry points of the same search (for per-stage timing): the coarse quantizer
+ * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing
+ * Iq [n][nprobe] / Dq [n][nprobe]; and the per-query inner-product table T3. */
+int ivfpq_coarse_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, float* Dq, void* stream);
+
+/* Merge S sorted partial results [S][n][k] into [n][k] on the device (the IndexShards
+ * merge, bench_gpu_1bn.py:605-616; host argsort merge, bench_multi_cpu_performance_OSDI.py:203-218). */
+int ivfpq_merge_topk_device(int S, int64_t n, int k, const float* Din, const int64_t* Iin, float* Dout,
+                            int64_t* Iout, void* stream);
+
+/* Per-stage device timing (the nsys stage split of MICRO_GPU_profiling/classify_stages.py:113-181,
+ * measured live with HIP events recorded on the launch stream around each stage).
+ * get_timing waits for the recorded events, returns per-stage sums in ms and launch counts
+ * for stages {0: coarse probe, 1: inner-product table T3, 2: fused LUT + scan + top-k}, and resets. */
+int ivfpq_set_timing(ivfpq_index* h, int on);
+int ivfpq_get_timing(ivfpq_index* h, double* ms, int64_t* count);
+
+/* Accessors (extract_FPGA_required_data.py:174-248; bench_polysemous_1bn.py:368). */
+int64_t ivfpq_ntotal(const ivfpq_index* h);
+int ivfpq_is_trained(const ivfpq_index* h);
+int ivfpq_get_dims(const ivfpq_index* h, int* d, int* nlist, int* M, int* nbits, int* metric);
+int ivfpq_get_centroids(const ivfpq_index* h, float* out);  /* [nlist][d]  (quantizer.xb) */
+int ivfpq_get_codebook(const ivfpq_index* h, float* out);   /* [M][256][d/M]  (pq.centroids) */
+/* Install trained quantizers (e.g. from a Faiss .index or another process); builds T1 on the GPU. */
+int ivfpq_set_trained(ivfpq_index* h, const float* centroids, const float* codebook);
+int ivfpq_get_list_sizes(const ivfpq_index* h, int64_t* out); /* [nlist] (invlists.list_size) */
+int ivfpq_get_list(const ivfpq_index* h, int list, uint8_t* codes, int64_t* ids); /* get_codes / get_ids */
+/* T1 = precomputed_table [nlist][M][256] (IndexIVFPQ::precomputed_table), copied to the host. */
+int ivfpq_get_precomputed_table(ivfpq_index* h, float* out);
+
+/* faiss.write_index / read_index (bench_polysemous_1bn.py:287-290; beir faiss_index.py:29)
+ * in this engine's own binary format ("CHIVFPQ1"). */
+int ivfpq_save(ivfpq_index* h, const char* path);
+int ivfpq_load(const char* path, int device, ivfpq_index** out);
+
+/* Brute-force exact L2 k-NN on the GPU (IndexFlatL2::search; the coarse-quantizer
+ * service of ralm/index_scanner/index_scanner.py:61-77).  Host buffers. */
+int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n, const float* x, int k, float* D,
+                      int64_t* I);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CHAMELEON_IVFPQ_H */

@@ -1,0 +1,316 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+The bar (BASELINE.json north_star): returned IDs bit-exact, L2 distances within
+1e-4 relative.  Because the kernels follow the oracle's fp32 operation order,
+these tests assert the stronger property where it holds: identical IDs AND
+identical distances (np.array_equal), with the 1e-4 tolerance asserted as well.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import faiss_amd as faiss
+from faiss_amd import datasets
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["d128_m16", "d64_m32_dsub2", "d96_m8_dsub12"]
+RTOL = 1e-4  # north_star distance tolerance
+
+
+def load_case(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, f"ivfpq_{name}.npz")))
+
+
+def gpu_index(z):
+    d, M, nlist = int(z["d"]), int(z["M"]), int(z["nlist"])
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+    ix.set_trained(z["centroids"], z["codebook"])
+    off = z["list_off"]
+    list_no = np.repeat(np.arange(nlist, dtype=np.int64), np.diff(off))
+    ix.add_preencoded(list_no, z["codes"], z["ids"])
+    ix.nprobe = int(z["nprobe"])
+    return ix
+
+
+def oracle_index(z):
+    d, M, nlist = int(z["d"]), int(z["M"]), int(z["nlist"])
+    ox = O.OracleIVFPQ(d, nlist, M)
+    ox.set_trained(z["centroids"], z["codebook"])
+    off = z["list_off"]
+    list_no = np.repeat(np.arange(nlist, dtype=np.int64), np.diff(off))
+    ox.add_preencoded(list_no, z["codes"], z["ids"])
+    ox.nprobe = int(z["nprobe"])
+    return ox
+
+
+def assert_same(D, I, Dr, Ir):
+    np.testing.assert_array_equal(I, Ir)
+    np.testing.assert_allclose(D, Dr, rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(D, Dr)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_search_matches_golden(golden_dir, case):
+    z = load_case(golden_dir, case)
+    ix = gpu_index(z)
+    D, I = ix.search(z["xq"], int(z["k"]))
+    assert_same(D, I, z["or_D"], z["or_I"])
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_coarse_and_tables_match_oracle(golden_dir, case):
+    import torch
+
+    z = load_case(golden_dir, case)
+    ix = gpu_index(z)
+    xq = torch.from_numpy(z["xq"]).cuda()
+    Dq, Iq = ix.coarse_device(xq)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(Iq.cpu().numpy(), z["or_lists"])
+    np.testing.assert_array_equal(Dq.cpu().numpy(), z["or_dis0"])
+    T1 = ix.precomputed_table.reshape(int(z["nlist"]), int(z["M"]), 256)
+    np.testing.assert_array_equal(T1, O.precompute_T1(z["centroids"], z["codebook"]))
+
+
+@pytest.mark.parametrize("k", [1, 7, 63, 64, 65, 100, 128, 129, 257, 600, 1024])
+def test_k_sweep(golden_dir, k):
+    z = load_case(golden_dir, "d128_m16")
+    ix, ox = gpu_index(z), oracle_index(z)
+    for nprobe in (1, 8):
+        ix.nprobe = ox.nprobe = nprobe
+        D, I = ix.search(z["xq"], k)
+        Dr, Ir = ox.search(z["xq"], k)
+        assert_same(D, I, Dr, Ir)
+
+
+def test_nprobe_above_nlist_is_clamped(golden_dir):
+    z = load_case(golden_dir, "d64_m32_dsub2")
+    ix, ox = gpu_index(z), oracle_index(z)
+    ix.nprobe = 100  # nlist = 32
+    ox.nprobe = 32
+    D, I = ix.search(z["xq"], 20)
+    Dr, Ir = ox.search(z["xq"], 20)
+    assert_same(D, I, Dr, Ir)
+
+
+def test_search_preassigned(golden_dir):
+    z = load_case(golden_dir, "d128_m16")
+    ix, ox = gpu_index(z), oracle_index(z)
+    lists = z["or_lists"].copy()
+    dis0 = z["or_dis0"].copy()
+    D, I = ix.search_preassigned(z["xq"], 10, lists, dis0)
+    assert_same(D, I, z["or_D"], z["or_I"])
+    # Dq = None means zeros (upstream contrib default)
+    D, I = faiss.contrib.ivf_tools.search_preassigned(ix, z["xq"], 10, lists)
+    Dr, Ir = ox.search_preassigned(z["xq"], 10, lists, None)
+    assert_same(D, I, Dr, Ir)
+    # skipped probes (-1) and the 8-argument Faiss form
+    lists[:, ::2] = -1
+    D = np.empty((lists.shape[0], 10), np.float32)
+    I = np.empty((lists.shape[0], 10), np.int64)
+    n = lists.shape[0]
+    ix.search_preassigned(n, faiss.swig_ptr(z["xq"]), 10, faiss.swig_ptr(lists), faiss.swig_ptr(dis0),
+                          faiss.swig_ptr(D), faiss.swig_ptr(I), False)
+    Dr, Ir = ox.search_preassigned(z["xq"], 10, lists, dis0)
+    assert_same(D, I, Dr, Ir)
+
+
+def test_padding_when_fewer_than_k():
+    rng = np.random.default_rng(5)
+    d, M, nlist = 32, 8, 16
+    cent = rng.normal(size=(nlist, d)).astype(np.float32) * 4
+    cb = rng.normal(size=(M, 256, d // M)).astype(np.float32)
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+    ix.set_trained(cent, cb)
+    ox = O.OracleIVFPQ(d, nlist, M)
+    ox.set_trained(cent, cb)
+    x = rng.normal(size=(40, d)).astype(np.float32) * 4
+    ix.add(x)
+    ox.add(x)
+    ix.nprobe = ox.nprobe = 2
+    q = rng.normal(size=(9, d)).astype(np.float32) * 4
+    D, I = ix.search(q, 30)
+    Dr, Ir = ox.search(q, 30)
+    assert_same(D, I, Dr, Ir)
+    assert (I == -1).any()
+    assert np.all(D[I == -1] == np.finfo(np.float32).max)
+    # empty index: all padding
+    ix.reset()
+    D, I = ix.search(q, 5)
+    assert np.all(I == -1)
+    # zero queries
+    D, I = ix.search(np.zeros((0, d), np.float32), 5)
+    assert D.shape == (0, 5)
+
+
+def test_exact_ties_ordered_by_label():
+    # duplicate vectors produce identical codes and distances: order is (dist, label)
+    rng = np.random.default_rng(11)
+    d, M, nlist = 32, 8, 4
+    cent = rng.normal(size=(nlist, d)).astype(np.float32)
+    cb = rng.normal(size=(M, 256, d // M)).astype(np.float32) * 0.3
+    base = rng.normal(size=(20, d)).astype(np.float32)
+    x = np.repeat(base, 40, axis=0)
+    ids = rng.permutation(x.shape[0]).astype(np.int64) * 3 + 1
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+    ix.set_trained(cent, cb)
+    ox = O.OracleIVFPQ(d, nlist, M)
+    ox.set_trained(cent, cb)
+    ix.add_with_ids(x, ids)
+    ox.add_with_ids(x, ids)
+    ix.nprobe = ox.nprobe = 4
+    D, I = ix.search(base[:6], 100)
+    Dr, Ir = ox.search(base[:6], 100)
+    assert_same(D, I, Dr, Ir)
+
+
+def test_train_and_encode_match_oracle():
+    x = datasets.synthetic_sift_like(6000, 32, seed=7, n_centres=50)
+    ix = faiss.IndexIVFPQ(None, 32, 16, 8, 8, device=0)
+    ix.niter_coarse, ix.niter_pq, ix.seed = 6, 5, 99
+    ix.train(x)
+    ox = O.OracleIVFPQ(32, 16, 8)
+    ox.train(x, niter_coarse=6, niter_pq=5, seed=99)
+    np.testing.assert_array_equal(ix.centroids(), ox.centroids)
+    np.testing.assert_array_equal(ix.codebook(), ox.codebook)
+    xa = datasets.synthetic_sift_like(3000, 32, seed=8, n_centres=50)
+    ix.add(xa)
+    ox.add(xa)
+    for l in range(16):
+        np.testing.assert_array_equal(ix.invlists.get_ids(l), ox.list_ids[l])
+        np.testing.assert_array_equal(ix.invlists.get_codes(l).reshape(-1, 8), ox.list_codes[l])
+    assert ix.ntotal == 3000
+    assert ix.quantizer.ntotal == 16
+
+
+def test_device_entry_points_match_host(golden_dir):
+    import torch
+
+    z = load_case(golden_dir, "d128_m16")
+    ix = gpu_index(z)
+    xq = torch.from_numpy(z["xq"]).cuda()
+    D, I = ix.search_device(xq, 10)
+    torch.cuda.synchronize()
+    assert_same(D.cpu().numpy(), I.cpu().numpy(), z["or_D"], z["or_I"])
+    Dq, Iq = ix.coarse_device(xq)
+    D2, I2 = ix.search_preassigned_device(xq, 10, Iq, Dq)
+    torch.cuda.synchronize()
+    assert_same(D2.cpu().numpy(), I2.cpu().numpy(), z["or_D"], z["or_I"])
+
+
+def test_merge_topk_device():
+    import torch
+
+    rng = np.random.default_rng(3)
+    S, n, k = 4, 33, 17
+    Ds = np.sort(rng.integers(0, 50, size=(S, n, k)).astype(np.float32), axis=2)
+    Is = rng.integers(0, 1000, size=(S, n, k)).astype(np.int64)
+    Is[:, :, -2:] = -1
+    Ds[:, :, -2:] = np.finfo(np.float32).max
+    # make each partial list sorted by (dist, id)
+    for s in range(S):
+        for q in range(n):
+            o = np.lexsort((np.where(Is[s, q] < 0, np.iinfo(np.int64).max, Is[s, q]), Ds[s, q]))
+            Ds[s, q], Is[s, q] = Ds[s, q][o], Is[s, q][o]
+    D, I = faiss.merge_topk_device(torch.from_numpy(Ds).cuda(), torch.from_numpy(Is).cuda())
+    D, I = D.cpu().numpy(), I.cpu().numpy()
+    for q in range(n):
+        dd = Ds[:, q].reshape(-1)
+        ii = Is[:, q].reshape(-1)
+        key = np.where(ii < 0, np.iinfo(np.int64).max, ii)
+        o = np.lexsort((key, dd))[:k]
+        np.testing.assert_array_equal(D[q], dd[o])
+        np.testing.assert_array_equal(I[q], ii[o])
+
+
+def test_flat_search_exact():
+    rng = np.random.default_rng(2)
+    xb = rng.integers(0, 20, size=(3000, 24)).astype(np.float32)
+    xq = rng.integers(0, 20, size=(50, 24)).astype(np.float32)
+    fl = faiss.IndexFlatL2(24, device=0)
+    fl.add(xb)
+    D, I = fl.search(xq, 12)
+    dd = ((xq[:, None, :].astype(np.float64) - xb[None, :, :]) ** 2).sum(-1)
+    for q in range(xq.shape[0]):
+        o = np.lexsort((np.arange(xb.shape[0]), dd[q]))[:12]
+        np.testing.assert_array_equal(I[q], o)
+        np.testing.assert_array_equal(D[q], dd[q][o].astype(np.float32))
+
+
+def test_save_load_roundtrip(tmp_path, golden_dir):
+    z = load_case(golden_dir, "d96_m8_dsub12")
+    ix = gpu_index(z)
+    p = tmp_path / "x.chivfpq"
+    faiss.write_index(ix, p)
+    iy = faiss.read_index(p, device=0)
+    assert iy.ntotal == ix.ntotal and iy.nprobe == ix.nprobe
+    D, I = iy.search(z["xq"], int(z["k"]))
+    assert_same(D, I, z["or_D"], z["or_I"])
+
+
+def test_index_factory_and_parameter_space(golden_dir):
+    z = load_case(golden_dir, "d128_m16")
+    ix = faiss.index_factory(128, "IVF64,PQ16")
+    ix.set_trained(z["centroids"], z["codebook"])
+    faiss.ParameterSpace().set_index_parameters(ix, "nprobe=8")
+    assert ix.nprobe == 8
+    assert ix.invlists.imbalance_factor() == 0.0
+
+
+def test_errors_are_runtime_errors(golden_dir):
+    z = load_case(golden_dir, "d128_m16")
+    ix = gpu_index(z)
+    with pytest.raises(RuntimeError):
+        ix.search(z["xq"][:, :64], 10)
+    with pytest.raises(RuntimeError):
+        ix.search(z["xq"], 0)
+    with pytest.raises(RuntimeError):
+        ix.search(z["xq"], 1025)
+    with pytest.raises(RuntimeError):
+        faiss.IndexIVFPQ(None, 128, 64, 16, 8, device=0).search(z["xq"], 5)  # untrained
+    with pytest.raises(RuntimeError):
+        faiss.IndexIVFPQ(None, 100, 64, 16, 8, device=0)  # d % M != 0
+
+
+def test_c2_full_size_bit_exact():
+    """C2 shape (SIFT1M-like, nlist=1024, M=16, nprobe=16, batch 1024): the GPU
+    engine's result equals the oracle's on the same trained index, and the
+    result is sorted with no duplicate labels."""
+    xt = datasets.synthetic_sift_like(100_000, 128, seed=4321)
+    xb = datasets.synthetic_sift_like(1_000_000, 128, seed=1234)
+    xq = datasets.synthetic_sift_like(1024, 128, seed=123)
+    ix = faiss.index_factory(128, "IVF1024,PQ16")
+    ix.niter_coarse, ix.niter_pq = 8, 8
+    ix.train(xt)
+    ix.add(xb)
+    ix.nprobe = 16
+    D, I = ix.search(xq, 10)
+    ox = O.OracleIVFPQ(128, 1024, 16)
+    ox.set_trained(ix.centroids(), ix.codebook())
+    # encode parity on a slice of the base set
+    lo, co = ox.encode(xb[:20000])
+    ids0 = np.concatenate([ix.invlists.get_ids(l) for l in range(1024)])
+    assert ids0.shape[0] == 1_000_000
+    for l in range(1024):
+        ox.list_ids[l] = ix.invlists.get_ids(l)
+        ox.list_codes[l] = ix.invlists.get_codes(l).reshape(-1, 16)
+    ox.ntotal = ix.ntotal
+    sel = ids0 < 20000
+    lists_all = np.concatenate([np.full(ix.invlists.list_size(l), l) for l in range(1024)])
+    codes_all = np.concatenate([ox.list_codes[l] for l in range(1024)])
+    o = np.argsort(ids0[sel])
+    np.testing.assert_array_equal(lists_all[sel][o], lo)
+    np.testing.assert_array_equal(codes_all[sel][o], co)
+    ox.nprobe = 16
+    Dr, Ir = ox.search(xq, 10)
+    assert_same(D, I, Dr, Ir)
+    assert np.all(np.diff(D, axis=1) >= 0)
+    for q in range(I.shape[0]):
+        assert len(set(I[q].tolist())) == 10
+    for k in (100, 1000):
+        D, I = ix.search(xq[:256], k)
+        Dr, Ir = ox.search(xq[:256], k)
+        assert_same(D, I, Dr, Ir)
