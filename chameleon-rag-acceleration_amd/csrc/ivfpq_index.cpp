@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -149,12 +150,45 @@ struct ivfpq_index {
   int64_t ntotal = 0;
   int64_t next_id = 0;
 
-  DevBuf d_cent, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off;
+  DevBuf d_cent, d_centT, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off;
   bool dirty = true;
   hipStream_t stream = nullptr;
   // scratch
   DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
+  // list-major scan plan workspaces
+  DevBuf p_first, p_slot, p_cnt, p_boff, p_it1, p_nit, p_D, p_I, p_tau;
+  bool query_major = false;
+  int debug = 0;  // IVFPQ_DEBUG: kernel timing ablations (wrong results)
+  std::string stamp_out;  // IVFPQ_STAMPS=<path>: dump phase-B in-kernel stamps (diagnostic)
+  DevBuf w_stamps;  // IVFPQ_SCAN=query selects the query-major kernel (A/B only)
   std::mutex mu;
+
+  ListPlan make_plan(int64_t nq, int np, int k) {
+    const int nloc = list_hi - list_lo;
+    const int G = list_scan_group(M, k);
+    ListPlan pl;
+    pl.cap = list_scan_cap(nq, np, nloc, G);
+    pl.grid = scan_lists_grid();
+    p_first.ensure(sizeof(int32_t) * nq);
+    p_slot.ensure(sizeof(int32_t) * nq * np);
+    p_cnt.ensure(sizeof(int32_t) * std::max(nloc, 1));
+    p_boff.ensure(sizeof(int32_t) * std::max(nloc, 1));
+    p_it1.ensure(sizeof(int32_t) * 16 * pl.cap);
+    p_nit.ensure(sizeof(int32_t) * 16);
+    p_D.ensure(sizeof(float) * nq * np * 4 * k);
+    p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
+    p_tau.ensure(sizeof(int32_t) * nq);
+    pl.first_probe = p_first.as<int32_t>();
+    pl.slot = p_slot.as<int32_t>();
+    pl.cnt = p_cnt.as<int32_t>();
+    pl.ioff = p_boff.as<int32_t>();
+    pl.recs = p_it1.as<int32_t>();
+    pl.n_items = p_nit.as<int32_t>();
+    pl.partD = p_D.as<float>();
+    pl.partI = p_I.as<int64_t>();
+    pl.tauq = p_tau.as<int32_t>();
+    return pl;
+  }
 
   // stage timing (HIP events recorded on the launch stream around each stage)
   enum Stage { ST_COARSE = 0, ST_TABLES = 1, ST_SCAN = 2, ST_N = 3 };
@@ -279,6 +313,14 @@ struct ivfpq_index {
     HIPCHECK(hipMemcpyAsync(d_cb.p, codebook.data(), sizeof(float) * codebook.size(), hipMemcpyHostToDevice,
                             stream));
     launch_row_norms(d_cent.as<float>(), nlist, d, d_cnorm.as<float>(), stream);
+    {  // transposed centroids [d][nlist] for the fused coarse kernel
+      std::vector<float> ct((size_t)nlist * d);
+      for (int l = 0; l < nlist; l++)
+        for (int t = 0; t < d; t++) ct[(size_t)t * nlist + l] = centroids[(size_t)l * d + t];
+      d_centT.ensure(sizeof(float) * ct.size());
+      HIPCHECK(hipMemcpyAsync(d_centT.p, ct.data(), sizeof(float) * ct.size(), hipMemcpyHostToDevice, stream));
+      HIPCHECK(hipStreamSynchronize(stream));
+    }
     launch_precompute_T1(d_cent.as<float>(), nlist, d, d_cb.as<float>(), M, ksub, d_T1.as<float>(), stream);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(stream));
@@ -292,10 +334,20 @@ struct ivfpq_index {
     const int64_t tot = off[nlist];
     std::vector<uint8_t> codes((size_t)tot * M);
     std::vector<int64_t> ids((size_t)tot);
+    // Device image: each list sorted by label (stable).  Results do not depend
+    // on the order inside a list, and label-sorted lists let the scan kernels
+    // rank candidates by code position instead of loading labels.
+    std::vector<int64_t> perm;
     for (int l = 0; l < nlist; l++) {
-      if (!lids[l].empty()) {
-        std::memcpy(codes.data() + off[l] * M, lcodes[l].data(), lcodes[l].size());
-        std::memcpy(ids.data() + off[l], lids[l].data(), sizeof(int64_t) * lids[l].size());
+      const int64_t n = (int64_t)lids[l].size();
+      if (!n) continue;
+      perm.resize(n);
+      for (int64_t i = 0; i < n; i++) perm[i] = i;
+      const int64_t* lid = lids[l].data();
+      std::stable_sort(perm.begin(), perm.end(), [lid](int64_t a, int64_t b) { return lid[a] < lid[b]; });
+      for (int64_t i = 0; i < n; i++) {
+        std::memcpy(codes.data() + (off[l] + i) * M, lcodes[l].data() + perm[i] * M, M);
+        ids[off[l] + i] = lid[perm[i]];
       }
     }
     d_codes.ensure(std::max<size_t>(16, codes.size()));
@@ -331,6 +383,21 @@ struct ivfpq_index {
     require(metric == IVFPQ_METRIC_L2, "only METRIC_L2 is served on the GPU");
   }
 
+  // coarse quantizer for c queries at x: nprobe nearest lists (fused kernel when
+  // the per-query distance rows fit in LDS, else distance matrix + select)
+  bool coarse_fused = true;  // IVFPQ_COARSE=split selects the two-kernel path (A/B)
+  void coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s) {
+    if (coarse_fused && nlist <= kCoarseFusedMax) {
+      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s);
+      return;
+    }
+    w_xn.ensure(sizeof(float) * c);
+    w_dist.ensure(sizeof(float) * c * nlist);
+    launch_row_norms(x, c, d, w_xn.as<float>(), s);
+    launch_l2_dist(x, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d, w_dist.as<float>(), s);
+    launch_select_rows(w_dist.as<float>(), c, nlist, np, dis, lists, s);
+  }
+
   // The full search on device pointers, on stream s.  Iq/Dq non-null = preassigned.
   void search_dev(int64_t n, const float* x, int k, float* D, int64_t* I, const int64_t* Iq, const float* Dq,
                   bool preassigned, hipStream_t s) {
@@ -338,7 +405,7 @@ struct ivfpq_index {
     upload_lists();
     if (n == 0) return;
     const int np = preassigned ? nprobe : eff_nprobe();
-    const size_t per_q = std::max<size_t>((size_t)nlist, (size_t)M * ksub) * 4;
+    const size_t per_q = std::max<size_t>(std::max<size_t>((size_t)nlist, (size_t)M * ksub) * 4, (size_t)np * k * 48);
     const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / per_q));
     w_T3.ensure(sizeof(float) * qc * M * ksub);
     if (!preassigned) {
@@ -357,10 +424,7 @@ struct ivfpq_index {
         dis0 = Dq ? Dq + q0 * np : nullptr;
       } else {
         const int tm = mark_begin(ST_COARSE, s);
-        launch_row_norms(xq, c, d, w_xn.as<float>(), s);
-        launch_l2_dist(xq, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d,
-                       w_dist.as<float>(), s);
-        launch_select_rows(w_dist.as<float>(), c, nlist, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s);
+        coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s);
         mark_end(tm, s);
         lists = w_lists.as<int64_t>();
         dis0 = w_dis0.as<float>();
@@ -382,10 +446,30 @@ struct ivfpq_index {
       a.M = M;
       a.list_lo = list_lo;
       a.list_hi = list_hi;
+      a.debug = debug;
       a.outD = D + q0 * k;
       a.outI = I + q0 * k;
       const int ts = mark_begin(ST_SCAN, s);
-      launch_scan_topk(a, s);
+      if (query_major) {
+        launch_scan_topk(a, s);
+      } else {
+        const size_t sb = sizeof(uint64_t) * scan_lists_grid() * kStampItems * kStampSlots;
+        if (!stamp_out.empty()) {
+          w_stamps.ensure(sb);
+          HIPCHECK(hipMemsetAsync(w_stamps.p, 0, sb, s));
+          a.stamps = w_stamps.as<uint64_t>();
+        }
+        launch_scan_lists(a, make_plan(c, np, k), s);
+        if (!stamp_out.empty()) {
+          std::vector<uint64_t> hs(sb / 8);
+          HIPCHECK(hipMemcpyAsync(hs.data(), w_stamps.p, sb, hipMemcpyDeviceToHost, s));
+          HIPCHECK(hipStreamSynchronize(s));
+          if (FILE* f = std::fopen(stamp_out.c_str(), "wb")) {
+            std::fwrite(hs.data(), 1, sb, f);
+            std::fclose(f);
+          }
+        }
+      }
       mark_end(ts, s);
       HIPCHECK(hipGetLastError());
     }
@@ -399,10 +483,7 @@ struct ivfpq_index {
     w_dist.ensure(sizeof(float) * qc * nlist);
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
-      launch_row_norms(x + q0 * d, c, d, w_xn.as<float>(), s);
-      launch_l2_dist(x + q0 * d, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d,
-                     w_dist.as<float>(), s);
-      launch_select_rows(w_dist.as<float>(), c, nlist, np, Dq + q0 * np, Iq + q0 * np, s);
+      coarse_launch(x + q0 * d, c, np, Dq + q0 * np, Iq + q0 * np, s);
       HIPCHECK(hipGetLastError());
     }
   }
@@ -489,6 +570,14 @@ int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivf
     h->list_hi = nlist;
     h->lcodes.resize(nlist);
     h->lids.resize(nlist);
+    const char* so = std::getenv("IVFPQ_STAMPS");
+    if (so) h->stamp_out = so;
+    const char* dbg = std::getenv("IVFPQ_DEBUG");
+    h->debug = dbg ? std::atoi(dbg) : 0;
+    const char* cs = std::getenv("IVFPQ_COARSE");
+    h->coarse_fused = !(cs && std::string(cs) == "split");
+    const char* sc = std::getenv("IVFPQ_SCAN");
+    h->query_major = sc && std::string(sc) == "query";
     h->init_stream();
     *out = h.release();
   });

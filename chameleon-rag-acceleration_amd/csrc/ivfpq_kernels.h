@@ -20,6 +20,14 @@ void launch_l2_dist(const float* x, const float* xn, int64_t nx, const float* c,
 void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, float* out_val, int64_t* out_col,
                         hipStream_t s);
 
+// Fused coarse quantizer for nlist <= kCoarseFusedMax: per query the distances
+// to all centroids (centT = centroids transposed [d][nlist], cn = |c|^2) and
+// the nprobe smallest (dis, list) pairs.  Same arithmetic as launch_l2_dist +
+// launch_select_rows.
+constexpr int kCoarseFusedMax = 8192;
+void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
+                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s);
+
 // T3[q][m][j] = <x_q[m], C_mj>  (Faiss AVX order)
 void launch_ip_table(const float* x, int64_t n, int d, const float* codebook, int M, int ksub, float* out,
                      hipStream_t s);
@@ -48,9 +56,44 @@ struct ScanArgs {
   int list_lo, list_hi;  // only lists in [list_lo, list_hi) are scanned (shard range)
   float* outD;           // [nq][k]
   int64_t* outI;         // [nq][k]
+  // threshold-seed mode of the query-major kernel: scan only probe first_probe[q]
+  // (skip the query if it is >= nprobe) and write the result to the partial slot
+  // partD/partI + (q * nprobe + first_probe[q]) * k.
+  const int32_t* first_probe = nullptr;
+  float* partD = nullptr;
+  int64_t* partI = nullptr;
+  int32_t* tauq = nullptr;  // seed mode also publishes each query's k-th distance here
+  int debug = 0;            // timing ablations only (wrong results): 1 = no phase-B top-k, 2 = no LUT reads
+  uint64_t* stamps = nullptr;  // diagnostic in-kernel s_memtime stamps (phase B), null in production
 };
+constexpr int kStampItems = 32;  // items stamped per phase-B workgroup
+constexpr int kStampSlots = 6;   // per item: start, LUT ready, scan done, merge done, n, cnt
 void launch_scan_topk(const ScanArgs& a, hipStream_t s);
 bool scan_supported_M(int M);
+
+// ---- Two-phase scan ------------------------------------------
+// Phase A (query-major k_scan_topk in seed mode): each query's first usable
+// probe, giving a per-query bound tau_q = its k-th distance.  Phase B
+// (list-major): work item = (inverted list, up to G queries probing it), every
+// other probe, admission dis <= tau_q.  A per-query merge combines the partials.
+struct ListPlan {
+  int32_t* first_probe;  // [nq]
+  int32_t* slot;         // [nq * nprobe]
+  int32_t* cnt;          // [nloc]
+  int32_t* ioff;         // [nloc]  first work item of each list
+  int32_t* recs;         // [cap][16] work item: list, count, size, offset(2), pairs(4), coarse dist(4)
+  int32_t* n_items;      // [1]
+  float* partD;          // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k
+  int64_t* partI;        // same shape: global code positions (-1 = none)
+  int32_t* tauq;         // [nq] running k-th distance bound per query (fp32 bits, atomicMin)
+  int cap;               // upper bound on the number of work items
+  int grid;              // persistent phase-B workgroups (multiple of 8)
+};
+int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
+// phase-B item-count upper bound for a batch (host side, to size ListPlan)
+int list_scan_cap(int64_t nq, int nprobe, int nloc, int G);
+void launch_scan_lists(const ScanArgs& a, const ListPlan& plan, hipStream_t s);
+int scan_lists_grid();  // persistent grid size for the device (2 workgroups per CU)
 
 // merge S sorted partial top-k lists [S][n][k] into [n][k]
 void launch_merge_topk(int S, int64_t n, int k, const float* Din, const int64_t* Iin, float* Dout, int64_t* Iout,

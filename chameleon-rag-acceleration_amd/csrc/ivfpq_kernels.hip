@@ -23,6 +23,8 @@
 #include <float.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include <hip/hip_runtime.h>
 
 #include "ivfpq_kernels.h"
@@ -102,12 +104,40 @@ __device__ __forceinline__ int64_t readlane_i64(int64_t v, int lane) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ float shfl_up1_f(float v) { return __shfl_up(v, 1, 64); }
+// Cross-lane moves on the VALU (DPP) instead of the LDS crossbar (ds_bpermute):
+// wave_shr:1 shifts the whole wave by one lane, lane 0 receiving `old`.
+__device__ __forceinline__ int dpp_shr1_i(int old, int v) { return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ float shr1_f(float old, float v) {
+  return __int_as_float(dpp_shr1_i(__float_as_int(old), __float_as_int(v)));
+}
+__device__ __forceinline__ int64_t shr1_i64(int64_t old, int64_t v) {
+  const uint64_t uo = (uint64_t)old, uv = (uint64_t)v;
+  const uint32_t lo = (uint32_t)dpp_shr1_i((int)(uint32_t)uo, (int)(uint32_t)uv);
+  const uint32_t hi = (uint32_t)dpp_shr1_i((int)(uint32_t)(uo >> 32), (int)(uint32_t)(uv >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
-__device__ __forceinline__ int64_t shfl_up1_i64(int64_t v) {
+// lane ^ J exchange: DPP for J <= 8, ds_swizzle for 16, bpermute for 32
+template <int CTRL>
+__device__ __forceinline__ int dmov(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int J>
+__device__ __forceinline__ int xor_i(int v) {
+  if constexpr (J == 1) return dmov<0xB1>(v);                  // quad_perm [1,0,3,2]
+  else if constexpr (J == 2) return dmov<0x4E>(v);             // quad_perm [2,3,0,1]
+  else if constexpr (J == 4) return dmov<0x1B>(dmov<0x141>(v));  // row_half_mirror, quad_perm [3,2,1,0]
+  else if constexpr (J == 8) return dmov<0x128>(v);            // row_ror:8
+  else if constexpr (J == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);  // swap 16
+  else return __shfl_xor(v, 32, 64);
+}
+template <int J>
+__device__ __forceinline__ float xor_f(float v) { return __int_as_float(xor_i<J>(__float_as_int(v))); }
+template <int J>
+__device__ __forceinline__ int64_t xor_i64(int64_t v) {
   const uint64_t u = (uint64_t)v;
-  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)u, 1, 64);
-  const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(u >> 32), 1, 64);
+  const uint32_t lo = (uint32_t)xor_i<J>((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)xor_i<J>((int)(uint32_t)(u >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
@@ -163,12 +193,8 @@ struct WaveTopK {
           cdd = readlane_f(d[r - 1], 63);
           cii = readlane_i64(id[r - 1], 63);
         }
-        float ud = shfl_up1_f(d[r]);
-        int64_t ui = shfl_up1_i64(id[r]);
-        if (lane == 0) {
-          ud = cdd;
-          ui = cii;
-        }
+        const float ud = shr1_f(cdd, d[r]);
+        const int64_t ui = shr1_i64(cii, id[r]);
         const int idx = r * 64 + lane;
         if (idx > pos) {
           d[r] = ud;
@@ -182,6 +208,64 @@ struct WaveTopK {
     }
   }
 };
+
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), src, 64);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)u, m, 64);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(u >> 32), m, 64);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Merge up to 64 candidates (one per lane; (inf, sentinel) = none) into a
+// single-row top-k: bitonic sort of the candidates, then the classic
+// reverse-min + bitonic merge against the sorted row.  Exchanges at strides
+// <= 8 are DPP moves, 16 a ds_swizzle, 32 a bpermute.
+template <int KK, int J>
+__device__ __forceinline__ void bitonic_step(float& cd, int64_t& ci, int lane) {
+  const float od = xor_f<J>(cd);
+  const int64_t oi = xor_i64<J>(ci);
+  const bool up = (lane & KK) == 0;
+  const bool lower = (lane & J) == 0;
+  const bool take = (lower == up) ? lexless(od, oi, cd, ci) : lexless(cd, ci, od, oi);
+  if (take) {
+    cd = od;
+    ci = oi;
+  }
+}
+template <int KK, int J>
+__device__ __forceinline__ void bitonic_steps(float& cd, int64_t& ci, int lane) {
+  if constexpr (J >= 1) {
+    bitonic_step<KK, J>(cd, ci, lane);
+    bitonic_steps<KK, J / 2>(cd, ci, lane);
+  }
+}
+template <int KK>
+__device__ __forceinline__ void bitonic_sort64(float& cd, int64_t& ci, int lane) {
+  if constexpr (KK <= 64) {
+    bitonic_steps<KK, KK / 2>(cd, ci, lane);
+    bitonic_sort64<KK * 2>(cd, ci, lane);
+  }
+}
+
+__device__ __forceinline__ void bulk_merge_row(WaveTopK<1>& tk, float cd, int64_t ci, int lane) {
+  bitonic_sort64<2>(cd, ci, lane);
+  const float rd = __shfl(cd, 63 - lane, 64);
+  const int64_t ri = shfl_i64(ci, 63 - lane);
+  if (lexless(rd, ri, tk.d[0], tk.id[0])) {
+    tk.d[0] = rd;
+    tk.id[0] = ri;
+  }
+  // ascending bitonic merge: KK = 128 keeps every lane "up"
+  bitonic_steps<128, 32>(tk.d[0], tk.id[0], lane);
+  tk.refresh_tau();
+}
 
 // ------------------------------------------------------------------ norms
 __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int d,
@@ -254,6 +338,113 @@ __global__ __launch_bounds__(256) void k_l2_dist(const float* __restrict__ x, co
   }
 }
 
+// ------------------------------------------------------- fused coarse probe
+// 4 queries per 256-thread workgroup.  Thread t owns centroids 4t..4t+3 of each
+// 1024-centroid block (float4 loads of the transposed centroids, coalesced) and
+// accumulates <x_q, c> as a k-ordered fmaf chain for the 4 queries (query
+// elements broadcast from LDS).  Distances land in LDS; wave w then selects
+// query w's nprobe nearest lists (same rule and arithmetic as k_l2_dist +
+// k_select_rows).
+constexpr int CQ = 4;
+
+template <int R>
+__global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
+                                                      const float* __restrict__ centT, const float* __restrict__ cn,
+                                                      int nlist, int nprobe, float* __restrict__ out_dis,
+                                                      int64_t* __restrict__ out_list) {
+  extern __shared__ __attribute__((aligned(16))) float cs_mem[];
+  float* xs = cs_mem;                       // [CQ][d]
+  float* xn = xs + CQ * d;                  // [CQ]
+  float* dist = xn + CQ;                    // [CQ][nlist]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t q0 = (int64_t)blockIdx.x * CQ;
+  for (int e = tid; e < CQ * d; e += 256) {
+    const int64_t q = q0 + e / d;
+    xs[e] = q < nq ? x[q0 * d + e] : 0.f;
+  }
+  __syncthreads();
+  if (tid < CQ) {
+    const float* xr = xs + tid * d;
+    xn[tid] = tree<K_NORM>([&](int t) { return xr[t]; }, [&](int t) { return xr[t]; }, d);
+  }
+  for (int cb0 = 0; cb0 < nlist; cb0 += 1024) {
+    const int c4 = cb0 + 4 * tid;  // first of this thread's 4 centroids
+    float acc[CQ][4];
+#pragma unroll
+    for (int qq = 0; qq < CQ; qq++)
+#pragma unroll
+      for (int u = 0; u < 4; u++) acc[qq][u] = 0.f;
+    if (c4 < nlist) {
+      const bool full = c4 + 4 <= nlist && (nlist & 3) == 0;
+      for (int kk = 0; kk < d; kk++) {
+        float cv[4];
+        if (full) {
+          const float4 v = *reinterpret_cast<const float4*>(centT + (int64_t)kk * nlist + c4);
+          cv[0] = v.x;
+          cv[1] = v.y;
+          cv[2] = v.z;
+          cv[3] = v.w;
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; u++) cv[u] = c4 + u < nlist ? centT[(int64_t)kk * nlist + c4 + u] : 0.f;
+        }
+#pragma unroll
+        for (int qq = 0; qq < CQ; qq++) {
+          const float xv = xs[qq * d + kk];
+#pragma unroll
+          for (int u = 0; u < 4; u++) acc[qq][u] = __builtin_fmaf(xv, cv[u], acc[qq][u]);
+        }
+      }
+    }
+    __syncthreads();  // xn ready
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int c = c4 + u;
+      if (c < nlist) {
+        const float cnv = cn[c];
+#pragma unroll
+        for (int qq = 0; qq < CQ; qq++) {
+          float dis = (xn[qq] + cnv) - 2.0f * acc[qq][u];
+          if (dis < 0.f) dis = 0.f;
+          dist[qq * nlist + c] = dis;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t q = q0 + wave;
+  if (q >= nq) return;
+  WaveTopK<R> tk;
+  tk.init(nprobe);
+  const float* drow = dist + wave * nlist;
+  for (int base = 0; base < nlist; base += 64) {
+    const int cix = base + lane;
+    const bool valid = cix < nlist;
+    const float v = valid ? drow[cix] : kInf;
+    const bool pass = valid && lexless(v, (int64_t)cix, tk.td, tk.ti);
+    const uint64_t mask = __ballot(pass);
+    if (!mask) continue;
+    if constexpr (R == 1) {
+      if (__popcll(mask) > 6) {
+        bulk_merge_row(tk, pass ? v : kInf, pass ? (int64_t)cix : kSentinelId, lane);
+        continue;
+      }
+    }
+    tk.insert(mask, v, (int64_t)cix, lane);
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int idx = r * 64 + lane;
+    if (idx < nprobe) {
+      const bool empty = tk.id[r] == kSentinelId;
+      out_dis[q * nprobe + idx] = empty ? FLT_MAX : tk.d[r];
+      out_list[q * nprobe + idx] = empty ? -1 : tk.id[r];
+    }
+  }
+}
+
 // ------------------------------------------------------------ row select
 template <int R>
 __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ dist, int64_t nrows, int ncols,
@@ -270,7 +461,14 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
     const float v = valid ? drow[cix] : kInf;
     const bool pass = valid && lexless(v, (int64_t)cix, tk.td, tk.ti);
     const uint64_t mask = __ballot(pass);
-    if (mask) tk.insert(mask, v, (int64_t)cix, lane);
+    if (!mask) continue;
+    if constexpr (R == 1) {
+      if (__popcll(mask) > 6) {
+        bulk_merge_row(tk, pass ? v : kInf, pass ? (int64_t)cix : kSentinelId, lane);
+        continue;
+      }
+    }
+    tk.insert(mask, v, (int64_t)cix, lane);
   }
 #pragma unroll
   for (int r = 0; r < R; r++) {
@@ -284,19 +482,19 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
 }
 
 // -------------------------------------------------------------- PQ tables
+// One workgroup per (query, sub-quantizer m): thread j computes T3[q][m][j]
+// (256 = ksub entries, coalesced store); q[m] is read once per workgroup.
 __global__ __launch_bounds__(256) void k_ip_table(const float* __restrict__ x, int64_t n, int d,
                                                   const float* __restrict__ cb, int M, int ksub,
                                                   float* __restrict__ out) {
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= n * M * ksub) return;
-  const int j = (int)(gid % ksub);
-  const int64_t t = gid / ksub;
-  const int m = (int)(t % M);
-  const int64_t q = t / M;
+  const int64_t q = blockIdx.y;
+  const int m = blockIdx.x;
+  const int j = threadIdx.x;
+  if (j >= ksub) return;
   const int dsub = d / M;
   const float* xq = x + q * d + m * dsub;
   const float* cw = cb + ((int64_t)m * ksub + j) * dsub;
-  out[gid] = tree<K_IP>([&](int u) { return xq[u]; }, [&](int u) { return cw[u]; }, dsub);
+  out[(q * M + m) * ksub + j] = tree<K_IP>([&](int u) { return xq[u]; }, [&](int u) { return cw[u]; }, dsub);
 }
 
 __global__ __launch_bounds__(256) void k_precompute_T1(const float* __restrict__ cent, int nlist, int d,
@@ -371,7 +569,11 @@ struct CodeWords {
   __device__ __forceinline__ uint32_t byte(int m) const { return (w[m >> 2] >> ((m & 3) * 8)) & 0xffu; }
 };
 
-template <int M, int R>
+// POSKEY: rank candidates by (distance, global code position) and translate
+// positions to labels only for the k survivors.  Valid when all candidates
+// come from ONE inverted list (seed mode): the device image of every list is
+// sorted by label, so position order equals label order inside a list.
+template <int M, int R, bool POSKEY>
 __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
   constexpr int LUTN = M * 256;  // fp32 entries per LUT
   constexpr int NV4 = M / 4;     // float4 per thread while forming the LUT
@@ -399,7 +601,12 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
   WaveTopK<R> tk;
   tk.init(k);
 
-  for (int p = 0; p < a.nprobe; ++p) {
+  int p_begin = 0, p_end = a.nprobe;
+  if (a.first_probe) {  // threshold-seed mode: only the first usable probe
+    p_begin = a.first_probe[q];
+    p_end = min(p_begin + 1, a.nprobe);
+  }
+  for (int p = p_begin; p < p_end; ++p) {
     const int64_t l = a.probe_list[q * a.nprobe + p];
     if (l < a.list_lo || l >= a.list_hi) continue;  // skipped probe (-1) or another shard's list
     const float d0 = a.probe_dis0 ? a.probe_dis0[q * a.nprobe + p] : 0.f;
@@ -437,13 +644,41 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
       }
       const bool maybe = valid && dis <= tk.td;
       int64_t id = kSentinelId;
-      if (maybe) id = lid[i];
+      if constexpr (POSKEY) {
+        id = beg + i;
+      } else {
+        if (maybe) id = lid[i];
+      }
       const bool pass = maybe && lexless(dis, id, tk.td, tk.ti);
       const uint64_t mask = __ballot(pass);
-      if (mask) tk.insert(mask, dis, id, lane);
+      if (!mask) continue;
+      if constexpr (R == 1) {
+        if (__popcll(mask) > 6) {
+          bulk_merge_row(tk, pass ? dis : kInf, pass ? id : kSentinelId, lane);
+          continue;
+        }
+      }
+      tk.insert(mask, dis, id, lane);
     }
   }
 
+  if (a.first_probe) {
+    // seed mode: every wave writes its own sorted list; any wave's k-th bounds
+    // the query's final k-th (phase B admission)
+    if (p_begin >= a.nprobe) return;
+    const int64_t o = ((q * a.nprobe + p_begin) * 4 + wave) * k;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int idx = r * 64 + lane;
+      if (idx < k) {
+        const bool empty = tk.id[r] == kSentinelId;
+        a.partD[o + idx] = empty ? FLT_MAX : tk.d[r];
+        a.partI[o + idx] = empty ? -1 : tk.id[r];
+      }
+    }
+    if (lane == 0 && tk.td < kInf) atomicMin(&a.tauq[q], __float_as_int(tk.td));
+    return;
+  }
   // ---- merge the four wave lists by rank
   __syncthreads();
   float* md = reinterpret_cast<float*>(smem);
@@ -482,7 +717,415 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
     if (rank < k) {
       const bool empty = vi == kSentinelId;
       a.outD[q * k + rank] = empty ? FLT_MAX : vd;
-      a.outI[q * k + rank] = empty ? -1 : vi;
+      a.outI[q * k + rank] = empty ? -1 : (POSKEY ? a.ids[vi] : vi);
+    }
+  }
+}
+
+
+// ===================================================== list-major two-phase scan
+// Bucketing: pairs (q, p) whose list is in the shard range and non-empty are
+// counted per list (global atomics), a single workgroup scans the counts into
+// bucket offsets and (list, bucket offset, count<=G) work items, then the pair
+// ids are scattered.  Order inside a bucket is arbitrary: results do not depend
+// on it (each (query, code) distance is computed independently and the final
+// order is (distance, label)).
+constexpr int PLAN_T = 1024;
+
+__device__ __forceinline__ bool usable_list(int64_t l, int lo, int hi, const int64_t* list_off) {
+  return l >= lo && l < hi && list_off[l + 1] > list_off[l];
+}
+
+// first usable probe per query (nprobe if none); also zeroes the per-list counters
+__global__ __launch_bounds__(256) void k_first_probe(const int64_t* __restrict__ lists, int64_t nq, int nprobe,
+                                                     const int64_t* __restrict__ list_off, int lo, int hi,
+                                                     ListPlan pl) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < (int64_t)(hi - lo)) pl.cnt[t] = 0;
+  if (t >= nq) return;
+  pl.tauq[t] = __float_as_int(kInf);
+  int fp = nprobe;
+  for (int p = 0; p < nprobe; p++)
+    if (usable_list(lists[t * nprobe + p], lo, hi, list_off)) {
+      fp = p;
+      break;
+    }
+  pl.first_probe[t] = fp;
+}
+
+__global__ __launch_bounds__(256) void k_bucket_count(const int64_t* __restrict__ lists, int64_t nq, int nprobe,
+                                                      const int64_t* __restrict__ list_off, int lo, int hi,
+                                                      ListPlan pl) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nq * nprobe) return;
+  const int64_t l = lists[i];
+  int s = -1;
+  if (usable_list(l, lo, hi, list_off) && (int)(i % nprobe) != pl.first_probe[i / nprobe])
+    s = atomicAdd(&pl.cnt[(int)(l - lo)], 1);
+  pl.slot[i] = s;
+}
+
+__global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, const int64_t* __restrict__ list_off,
+                                                        ListPlan pl) {
+  __shared__ int32_t part[PLAN_T];
+  const int tid = threadIdx.x;
+  const int nloc = hi - lo;
+  const int chunk = (nloc + PLAN_T - 1) / PLAN_T;
+  const int j0 = min(nloc, tid * chunk), j1 = min(nloc, j0 + chunk);
+  int si = 0;
+  for (int j = j0; j < j1; j++) si += (pl.cnt[j] + G - 1) / G;
+  part[tid] = si;
+  __syncthreads();
+  for (int off = 1; off < PLAN_T; off <<= 1) {
+    const int a = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += a;
+    __syncthreads();
+  }
+  int io = part[tid] - si;
+  for (int j = j0; j < j1; j++) {
+    const int c = pl.cnt[j];
+    pl.ioff[j] = io;
+    const int nit = (c + G - 1) / G;
+    const int64_t beg = nit ? list_off[lo + j] : 0;
+    const int32_t sz = nit ? (int32_t)(list_off[lo + j + 1] - beg) : 0;
+    for (int t = 0; t < nit; t++) {
+      int32_t* r = pl.recs + (int64_t)(io + t) * 16;
+      r[0] = lo + j;
+      r[1] = min(G, c - t * G);
+      r[2] = sz;
+      r[3] = (int32_t)(uint32_t)(uint64_t)beg;
+      r[4] = (int32_t)(uint32_t)((uint64_t)beg >> 32);
+    }
+    io += nit;
+  }
+  if (tid == PLAN_T - 1) pl.n_items[0] = part[PLAN_T - 1];
+  if (tid < 8) pl.n_items[1 + tid] = 0;  // per-XCD-group work counters of phase B
+}
+
+// scatter each phase-B pair id into its work item record
+__global__ __launch_bounds__(256) void k_bucket_scatter(const int64_t* __restrict__ lists,
+                                                        const float* __restrict__ dis0, int64_t nq, int nprobe, int lo,
+                                                        int G, ListPlan pl) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nq * nprobe) return;
+  const int s = pl.slot[i];
+  if (s < 0) return;
+  const int item = pl.ioff[(int)(lists[i] - lo)] + s / G;
+  int32_t* r = pl.recs + (int64_t)item * 16;
+  r[5 + s % G] = (int32_t)i;
+  r[9 + s % G] = __float_as_int(dis0 ? dis0[i] : 0.f);
+}
+
+template <int G>
+struct LutVec;
+template <>
+struct LutVec<1> {
+  using T = float;
+};
+template <>
+struct LutVec<2> {
+  using T = float2;
+};
+template <>
+struct LutVec<4> {
+  using T = float4;
+};
+
+__device__ __forceinline__ float comp(float v, int) { return v; }
+__device__ __forceinline__ float comp(float2 v, int g) { return g == 0 ? v.x : v.y; }
+__device__ __forceinline__ float comp(float4 v, int g) { return g == 0 ? v.x : g == 1 ? v.y : g == 2 ? v.z : v.w; }
+__device__ __forceinline__ void setc(float& o, int, float x) { o = x; }
+__device__ __forceinline__ void setc(float2& o, int g, float x) {
+  if (g == 0) o.x = x; else o.y = x;
+}
+__device__ __forceinline__ void setc(float4& o, int g, float x) {
+  if (g == 0) o.x = x; else if (g == 1) o.y = x; else if (g == 2) o.z = x; else o.w = x;
+}
+
+// Phase B.  Persistent workgroups; each walks the work items of its XCD group
+// (blocks b and b+8 share an XCD, so the consecutive items of one list -- same
+// T1 row, same codes -- stay on one L2).  A work item is (list l, up to G
+// queries); the G LUTs are interleaved per entry ([m][j][g]) so one
+// ds_read_b{32,64,128} returns the G lookups of a code and the bank conflicts of
+// the random 8-bit gathers are paid once per G lookups.
+// Each wave issues all its code loads of a batch (up to J codes per lane) at
+// once, with clamped addresses so the load sequence is branch-free and the
+// compiler's vmcnt waits stay counted.  Candidates (dis <= min(own k-th,
+// tau_q)) go to a per-wave LDS queue that one compact loop drains into the
+// wave's per-query top-k, ranked by (distance, code position): device lists are
+// label-sorted, so this equals (distance, label) inside a list.  tau_q is shared
+// across workgroups through global atomicMin (any k real candidates bound the
+// final k-th; a stale read is only a looser bound).
+constexpr int QCAP = 256;  // per-wave candidate queue entries
+
+template <int M, int G, int R, int J>
+__global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
+  using V = typename LutVec<G>::T;
+  constexpr int LUTN = M * 256;
+  constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table
+  constexpr int KP = R * 64;
+  constexpr int LUT_BYTES = LUTN * (int)sizeof(V);
+  constexpr int MERGE_BYTES = 4 * KP * 12;
+  constexpr int SMEM = LUT_BYTES > MERGE_BYTES ? LUT_BYTES : MERGE_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  __shared__ float qd[4][QCAP];
+  __shared__ int32_t qi[4][QCAP];  // (code position << 2) | g
+  V* lut = reinterpret_cast<V*>(smem);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int k = a.k;
+  const int n_items = pl.n_items[0];
+  // a.debug & 8: one global work counter (A/B against per-XCD-group counters)
+  const bool global_q = (a.debug & 8) != 0;
+  const int per = global_q ? n_items : (n_items + 7) >> 3;
+  const int grp = global_q ? 0 : (blockIdx.x & 7);
+  const int c0 = grp * per;
+  const int c1 = min(n_items, c0 + per);
+  const uint64_t lanemask_lt = (1ull << lane) - 1;
+
+  int it_no = 0;
+  auto stamp = [&](int slot, uint64_t v) {
+    if (a.stamps && tid == 0 && it_no < kStampItems)
+      a.stamps[((int64_t)blockIdx.x * kStampItems + it_no) * kStampSlots + slot] = v;
+  };
+  // dynamic work fetching inside the XCD group (items vary from 1 to ~3k codes)
+  __shared__ int s_next;
+  int* ctr = pl.n_items + 1 + grp;
+  if (tid == 0) s_next = c0 + atomicAdd(ctr, 1);
+  __syncthreads();
+  for (int idx = s_next; idx < c1; idx = s_next, it_no++) {
+    __syncthreads();  // everyone has read s_next
+    if (tid == 0) s_next = c0 + atomicAdd(ctr, 1);  // consumed after this item
+    stamp(0, __builtin_amdgcn_s_memtime());
+    // one self-contained record: no dependent metadata loads
+    const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)idx * 16);
+    const int4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+    const int64_t l = r0.x;
+    const int cnt = r0.y;
+    const int n = r0.z;
+    const int64_t beg = (int64_t)(((uint64_t)(uint32_t)r1.x << 32) | (uint32_t)r0.w);
+    int pair[G];
+    int64_t qix[G];
+    float d0[G], bound[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      const int pr = g == 0 ? r1.y : g == 1 ? r1.z : g == 2 ? r1.w : r2.x;
+      const int db = g == 0 ? r2.y : g == 1 ? r2.z : g == 2 ? r2.w : r3.x;
+      pair[g] = g < cnt ? pr : 0;
+      qix[g] = pair[g] / a.nprobe;
+      d0[g] = __int_as_float(db);
+    }
+    // every load of the item is issued before anything waits: T1/T3 rows,
+    // the query bounds and this wave's first batch of codes
+    float4 t1v[NV];
+    float4 t3v[G][NV];
+    {
+      const float4* T1l = reinterpret_cast<const float4*>(a.T1 + l * LUTN);
+#pragma unroll
+      for (int e = 0; e < NV; e++) t1v[e] = T1l[e * 256 + tid];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const float4* T3q = reinterpret_cast<const float4*>(a.T3 + qix[g] * LUTN);
+#pragma unroll
+        for (int e = 0; e < NV; e++) t3v[g][e] = T3q[e * 256 + tid];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) bound[g] = g < cnt ? __int_as_float(pl.tauq[qix[g]]) : -kInf;
+    const uint8_t* lc = a.codes + beg * M;
+    CodeWords<M> cw[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const int i = j * 256 + wave * 64 + lane;
+      cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
+    }
+    __syncthreads();  // the previous item is done with the LDS
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+      const int v = e * 256 + tid;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        V o;
+#pragma unroll
+        for (int g = 0; g < G; g++) setc(o, g, comp(t1v[e], c) + (-2.0f * comp(t3v[g][e], c)));
+        lut[4 * v + c] = o;
+      }
+    }
+    __syncthreads();
+    stamp(1, __builtin_amdgcn_s_memtime());
+
+    WaveTopK<R> tk[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) tk[g].init(k);
+    int qn = 0;  // this wave's queue fill (wave-uniform)
+
+    for (int base = 0; base < n; base += 256 * J) {
+      if (base > 0) {
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+          const int i = base + j * 256 + wave * 64 + lane;
+          cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
+        }
+      }
+      int jdone = 0;
+      while (jdone < J && base + jdone * 256 < n) {
+        int jstop = J;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+          const int i = base + j * 256 + wave * 64 + lane;
+          const bool run = j >= jdone && jstop == J && base + j * 256 < n;  // wave-uniform
+          if (run && qn + 64 * G > QCAP) jstop = j;  // queue could overflow: drain first
+          if (run && jstop == J) {
+            const bool valid = i < n;
+            float dis[G];
+#pragma unroll
+            for (int g = 0; g < G; g++) dis[g] = d0[g];
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+              const V v = lut[m * 256 + cw[j].byte(m)];
+#pragma unroll
+              for (int g = 0; g < G; g++) dis[g] = dis[g] + comp(v, g);
+            }
+            if (a.debug & 1) {
+#pragma unroll
+              for (int g = 0; g < G; g++) asm volatile("" ::"v"(dis[g]));
+            } else {
+#pragma unroll
+              for (int g = 0; g < G; g++) {
+                const bool pass = valid && dis[g] <= bound[g];
+                const uint64_t mask = __ballot(pass);
+                if (pass) {
+                  const int sl = qn + __popcll(mask & lanemask_lt);
+                  qd[wave][sl] = dis[g];
+                  qi[wave][sl] = (i << 2) | g;
+                }
+                qn += __popcll(mask);
+              }
+            }
+          }
+        }
+        jdone = jstop;
+        if (qn > 0) {  // drain the queue into the per-query top-k lists
+          for (int b0 = 0; b0 < qn; b0 += 64) {
+            const int e = b0 + lane;
+            const float cd = e < qn ? qd[wave][e] : kInf;
+            const int ci = e < qn ? qi[wave][e] : 0;
+            const int64_t pos = ci >> 2;
+            const int cg = ci & 3;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              const bool p = e < qn && cg == g && lexless(cd, pos, tk[g].td, tk[g].ti);
+              const uint64_t mk = __ballot(p);
+              if (mk) {
+                if constexpr (R == 1) {
+                  if (__popcll(mk) > 6)
+                    bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : kSentinelId, lane);
+                  else
+                    tk[g].insert(mk, cd, pos, lane);
+                } else {
+                  tk[g].insert(mk, cd, pos, lane);
+                }
+                bound[g] = fminf(bound[g], tk[g].td);
+              }
+            }
+          }
+          qn = 0;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (g < cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
+          }
+        }
+      }
+    }
+
+    stamp(2, __builtin_amdgcn_s_memtime());
+    stamp(4, (uint64_t)n);
+    stamp(5, (uint64_t)cnt);
+    // each wave writes its own sorted partial list per query (no in-workgroup merge)
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      if (g >= cnt) continue;
+      const int64_t o = ((int64_t)pair[g] * 4 + wave) * k;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const int ix = r * 64 + lane;
+        if (ix < k) {
+          const bool empty = tk[g].id[r] == kSentinelId;
+          pl.partD[o + ix] = empty ? FLT_MAX : tk[g].d[r];
+          pl.partI[o + ix] = empty ? -1 : beg + tk[g].id[r];  // global code position
+        }
+      }
+    }
+    stamp(3, __builtin_amdgcn_s_memtime());
+    __syncthreads();  // s_next is visible
+  }
+}
+
+// Per query (one wave): merge the per-wave partial lists of every scanned
+// probe ([probe][4 waves][k], sorted by (distance, position)).  All entries are
+// fetched in batches of 64 lanes x B loads (one round trip per batch); labels
+// are looked up only for entries that can still enter the top-k.
+template <int R>
+__global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
+  constexpr int B = 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= a.nq) return;
+  const int k = a.k;
+  const int np = a.nprobe;
+  const int fp = pl.first_probe[q];
+  WaveTopK<R> tk;
+  tk.init(k);
+  const int per_probe = 4 * k;
+  const int total = np * per_probe;
+  const float* pd = pl.partD + q * (int64_t)total;
+  const int64_t* pi = pl.partI + q * (int64_t)total;
+  for (int e0 = 0; e0 < total; e0 += 64 * B) {
+    float d[B];
+    int64_t pos[B];
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const int e = e0 + b * 64 + lane;
+      d[b] = kInf;
+      pos[b] = -1;
+      if (e < total) {
+        const int p = e / per_probe;
+        const int64_t l = a.probe_list[q * np + p];
+        const bool scanned = p < np && l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l] &&
+                             (p == fp || fp < np);
+        if (scanned) {
+          d[b] = pd[e];
+          pos[b] = pi[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+      const bool maybe = pos[b] >= 0 && d[b] <= tk.td;
+      int64_t id = kSentinelId;
+      if (maybe) id = a.ids[pos[b]];
+      const bool pass = maybe && lexless(d[b], id, tk.td, tk.ti);
+      const uint64_t mask = __ballot(pass);
+      if (!mask) continue;
+      if constexpr (R == 1) {
+        if (__popcll(mask) > 6) {
+          bulk_merge_row(tk, pass ? d[b] : kInf, pass ? id : kSentinelId, lane);
+          continue;
+        }
+      }
+      tk.insert(mask, d[b], id, lane);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int idx = r * 64 + lane;
+    if (idx < k) {
+      const bool empty = tk.id[r] == kSentinelId;
+      a.outD[q * k + idx] = empty ? FLT_MAX : tk.d[r];
+      a.outI[q * k + idx] = empty ? -1 : tk.id[r];
     }
   }
 }
@@ -557,10 +1200,34 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
   }
 }
 
+void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
+                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s) {
+  if (nq <= 0) return;
+  const size_t smem = sizeof(float) * (CQ * d + CQ + (size_t)CQ * nlist);
+  const dim3 grid(nblocks(nq, CQ));
+  static bool attr_set = false;
+  if (!attr_set) {  // dynamic LDS above 64 KiB must be opted into
+    const int lim = 160 * 1024;
+    (void)hipFuncSetAttribute((const void*)k_coarse_fused<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void*)k_coarse_fused<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void*)k_coarse_fused<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void*)k_coarse_fused<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    (void)hipFuncSetAttribute((const void*)k_coarse_fused<16>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    attr_set = true;
+  }
+  switch (rows_for(nprobe)) {
+    case 1: hipLaunchKernelGGL(k_coarse_fused<1>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
+    case 2: hipLaunchKernelGGL(k_coarse_fused<2>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
+    case 4: hipLaunchKernelGGL(k_coarse_fused<4>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
+    case 8: hipLaunchKernelGGL(k_coarse_fused<8>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
+    default: hipLaunchKernelGGL(k_coarse_fused<16>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
+  }
+}
+
 void launch_ip_table(const float* x, int64_t n, int d, const float* cb, int M, int ksub, float* out,
                      hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_ip_table, dim3(nblocks(n * M * ksub, 256)), dim3(256), 0, s, x, n, d, cb, M, ksub, out);
+  hipLaunchKernelGGL(k_ip_table, dim3((unsigned)M, (unsigned)n), dim3(256), 0, s, x, n, d, cb, M, ksub, out);
 }
 
 void launch_precompute_T1(const float* cent, int nlist, int d, const float* cb, int M, int ksub, float* T1,
@@ -582,11 +1249,11 @@ template <int M>
 static void launch_scan_M(const ScanArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)a.nq);
   switch (rows_for(a.k)) {
-    case 1: hipLaunchKernelGGL((k_scan_topk<M, 1>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_scan_topk<M, 2>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_scan_topk<M, 4>), grid, dim3(256), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_scan_topk<M, 8>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((k_scan_topk<M, 16>), grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_scan_topk<M, 1, false>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_scan_topk<M, 2, false>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_scan_topk<M, 4, false>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_scan_topk<M, 8, false>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((k_scan_topk<M, 16, false>), grid, dim3(256), 0, s, a); break;
   }
 }
 
@@ -598,6 +1265,76 @@ void launch_scan_topk(const ScanArgs& a, hipStream_t s) {
     case 32: launch_scan_M<32>(a, s); break;
     case 48: launch_scan_M<48>(a, s); break;
     case 64: launch_scan_M<64>(a, s); break;
+    default: break;
+  }
+}
+
+int list_scan_group(int M, int k) {
+  const int R = rows_for(k);
+  int G = 4;
+  while (G > 1 && (M * 1024 * G > 65536 || G * R > 16)) G >>= 1;
+  return G;
+}
+
+int list_scan_cap(int64_t nq, int nprobe, int nloc, int G) {
+  const int64_t p1 = nq * (nprobe > 1 ? nprobe - 1 : 0);
+  const int64_t v = std::min<int64_t>(nloc, p1) + (p1 + G - 1) / G + 8;
+  return (int)(((v + 7) / 8) * 8);
+}
+
+template <int M, int R>
+static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
+  constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 16) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 16) ? 2 : 1;
+  constexpr int J = M <= 8 ? 8 : M <= 16 ? 4 : 2;  // codes per lane per batch (register budget)
+  ScanArgs seed = a;
+  seed.first_probe = pl.first_probe;
+  seed.partD = pl.partD;
+  seed.partI = pl.partI;
+  seed.tauq = pl.tauq;
+  hipLaunchKernelGGL((k_scan_topk<M, R, true>), dim3((unsigned)a.nq), dim3(256), 0, s, seed);
+  hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+  hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
+}
+
+int scan_lists_grid() {
+  static int grid = 0;
+  if (!grid) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = std::max(8, (2 * cus + 7) / 8 * 8);
+  }
+  return grid;
+}
+
+template <int M>
+static void launch_lists_M(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
+  switch (rows_for(a.k)) {
+    case 1: launch_lists_MR<M, 1>(a, pl, s); break;
+    case 2: launch_lists_MR<M, 2>(a, pl, s); break;
+    case 4: launch_lists_MR<M, 4>(a, pl, s); break;
+    case 8: launch_lists_MR<M, 8>(a, pl, s); break;
+    default: launch_lists_MR<M, 16>(a, pl, s); break;
+  }
+}
+
+void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
+  if (a.nq <= 0) return;
+  const int G = list_scan_group(a.M, a.k);
+  const int64_t npairs = a.nq * a.nprobe;
+  const int nloc = a.list_hi - a.list_lo;
+  hipLaunchKernelGGL(k_first_probe, dim3(nblocks(std::max<int64_t>(a.nq, (int64_t)nloc), 256)), dim3(256), 0, s,
+                     a.probe_list, a.nq, a.nprobe, a.list_off, a.list_lo, a.list_hi, pl);
+  hipLaunchKernelGGL(k_bucket_count, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.nq, a.nprobe,
+                     a.list_off, a.list_lo, a.list_hi, pl);
+  hipLaunchKernelGGL(k_bucket_plan, dim3(1), dim3(PLAN_T), 0, s, a.list_lo, a.list_hi, G, a.list_off, pl);
+  hipLaunchKernelGGL(k_bucket_scatter, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.probe_dis0,
+                     a.nq, a.nprobe, a.list_lo, G, pl);
+  switch (a.M) {
+    case 8: launch_lists_M<8>(a, pl, s); break;
+    case 16: launch_lists_M<16>(a, pl, s); break;
+    case 32: launch_lists_M<32>(a, pl, s); break;
+    case 48: launch_lists_M<48>(a, pl, s); break;
+    case 64: launch_lists_M<64>(a, pl, s); break;
     default: break;
   }
 }

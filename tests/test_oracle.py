@@ -1,0 +1,139 @@
+"""CPU oracle pinning (no GPU): the oracle against the committed golden vectors,
+the reference's own NumPy IVF-PQ search and the FPGA LUT known-answer test."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+CASES = ["d128_m16", "d64_m32_dsub2", "d96_m8_dsub12"]
+
+
+def load(golden_dir, name):
+    return dict(np.load(os.path.join(golden_dir, name)))
+
+
+def oracle_from(z):
+    d, M, nlist = int(z["d"]), int(z["M"]), int(z["nlist"])
+    ox = O.OracleIVFPQ(d, nlist, M)
+    ox.set_trained(z["centroids"], z["codebook"])
+    list_no = np.repeat(np.arange(nlist, dtype=np.int64), np.diff(z["list_off"]))
+    ox.add_preencoded(list_no, z["codes"], z["ids"])
+    ox.nprobe = int(z["nprobe"])
+    return ox
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_reproduces_golden_bit_exact(golden_dir, case):
+    z = load(golden_dir, f"ivfpq_{case}.npz")
+    ox = oracle_from(z)
+    dis, lists = O.coarse_search(z["xq"], z["centroids"], int(z["nprobe"]))
+    np.testing.assert_array_equal(lists, z["or_lists"])
+    np.testing.assert_array_equal(dis, z["or_dis0"])
+    D, I = ox.search(z["xq"], int(z["k"]))
+    np.testing.assert_array_equal(I, z["or_I"])
+    np.testing.assert_array_equal(D, z["or_D"])
+    # thread count must not change results (queries are independent)
+    D1, I1 = ox.search(z["xq"], int(z["k"]), nthreads=1)
+    np.testing.assert_array_equal(I1, I)
+    np.testing.assert_array_equal(D1, D)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_matches_reference_notebook(golden_dir, case):
+    """IVFPQ_1B_search.ipynb cell 20 (run by tests/golden/make_golden.py) uses the
+    residual LUT with float64 accumulation.  Distances agree within the
+    north-star tolerance; labels agree except inside exact/near-tie groups,
+    which the notebook orders by scan order and the oracle by label."""
+    z = load(golden_dir, f"ivfpq_{case}.npz")
+    D, I = z["or_D"].astype(np.float64), z["or_I"]
+    nbD, nbI = z["nb_dists"], z["nb_ids"]
+    np.testing.assert_allclose(D, nbD, rtol=1e-4)
+    for q in range(I.shape[0]):
+        for j in np.where(I[q] != nbI[q])[0]:
+            tol = 1e-4 * max(1.0, abs(D[q, j]))
+            same_group = np.abs(D[q] - D[q, j]) <= tol
+            boundary_tie = abs(D[q, -1] - D[q, j]) <= tol
+            assert nbI[q, j] in I[q][same_group] or boundary_tie, (case, q, j)
+    assert (I == nbI).mean() > 0.2  # sanity: the generator has many exact ties (duplicate codes)
+
+
+@pytest.mark.parametrize("M", [32, 16])
+def test_lut_known_answer(golden_dir, M):
+    """FPGA LUT KAT (LUT_construction_PE_D128_M32/src/host.cpp:44-109): with
+    integer inputs the Faiss table route T1 + (-2) T3 plus |r_m|^2 equals the
+    residual LUT exactly."""
+    z = load(golden_dir, "lut_kat.npz")
+    q, c = z["query"], z["center"]
+    cb = z[f"codebook_M{M}"]
+    kat = z[f"lut_M{M}"]  # [256][M]
+    T1 = O.precompute_T1(c[None, :], cb)[0]  # [M][256]
+    T3 = O.ip_table(q[None, :], cb)[0]
+    lut = T1 + (-2.0 * T3).astype(np.float32)
+    r = (q - c).reshape(M, -1)
+    rn = (r.astype(np.float64) ** 2).sum(1).astype(np.float32)
+    np.testing.assert_array_equal(lut + rn[:, None], kat.T)
+
+
+def test_tree_reduction_order():
+    rng = np.random.default_rng(1)
+    f = np.float32
+    for d in (1, 2, 3, 4, 7, 8, 12, 16, 24):
+        x = rng.standard_normal(d).astype(np.float32)
+        y = rng.standard_normal(d).astype(np.float32)
+        p = (x * y).astype(np.float32)
+        a8 = np.zeros(8, np.float32)
+        i = 0
+        while i + 8 <= d:
+            a8 = (a8 + p[i:i + 8]).astype(np.float32)
+            i += 8
+        a4 = (a8[4:] + a8[:4]).astype(np.float32)
+        if i + 4 <= d:
+            a4 = (a4 + p[i:i + 4]).astype(np.float32)
+            i += 4
+        for j in range(d - i):
+            a4[j] = f(a4[j] + p[i + j])
+        ref = f(f(a4[0] + a4[1]) + f(a4[2] + a4[3]))
+        assert O.tree(x, y, 0) == ref, d
+
+
+def test_kmeans_deterministic_and_train_encode():
+    from faiss_amd import datasets
+
+    x = datasets.synthetic_sift_like(3000, 16, seed=3, n_centres=20)
+    c1 = O.kmeans(x, 16, 5, 7)
+    c2 = O.kmeans(x, 16, 5, 7, nthreads=1)
+    np.testing.assert_array_equal(c1, c2)
+    ox = O.OracleIVFPQ(16, 8, 4)
+    ox.train(x, niter_coarse=4, niter_pq=4, seed=5)
+    lists, codes = ox.encode(x[:200])
+    assert lists.min() >= 0 and lists.max() < 8
+    assert codes.shape == (200, 4)
+    ox.add(x)
+    assert ox.ntotal == 3000
+    ox.nprobe = 8
+    D, I = ox.search(x[:10], 5)
+    assert np.all(np.diff(D, axis=1) >= 0)
+
+
+def test_preassigned_zero_coarse_default(golden_dir):
+    z = load(golden_dir, "ivfpq_d128_m16.npz")
+    ox = oracle_from(z)
+    D0, I0 = ox.search_preassigned(z["xq"], 10, z["or_lists"], None)
+    Dz, Iz = ox.search_preassigned(z["xq"], 10, z["or_lists"], np.zeros_like(z["or_dis0"]))
+    np.testing.assert_array_equal(I0, Iz)
+    np.testing.assert_array_equal(D0, Dz)
+    D, I = ox.search_preassigned(z["xq"], 10, z["or_lists"], z["or_dis0"])
+    np.testing.assert_array_equal(I, z["or_I"])
+
+
+def test_padding_fewer_than_k():
+    rng = np.random.default_rng(0)
+    ox = O.OracleIVFPQ(16, 4, 4)
+    ox.set_trained(rng.standard_normal((4, 16)), rng.standard_normal((4, 256, 4)))
+    ox.add(rng.standard_normal((5, 16)).astype(np.float32))
+    ox.nprobe = 4
+    D, I = ox.search(rng.standard_normal((3, 16)).astype(np.float32), 8)
+    assert np.all(I[:, 5:] == -1)
+    assert np.all(D[:, 5:] == np.finfo(np.float32).max)
