@@ -169,6 +169,7 @@ struct ivfpq_index {
     ListPlan pl;
     pl.cap = list_scan_cap(nq, np, nloc, G);
     pl.grid = scan_lists_grid();
+    pl.seed = (debug & 64) ? 0 : 1;
     p_first.ensure(sizeof(int32_t) * nq);
     p_slot.ensure(sizeof(int32_t) * nq * np);
     p_cnt.ensure(sizeof(int32_t) * std::max(nloc, 1));
@@ -314,9 +315,10 @@ struct ivfpq_index {
                             stream));
     launch_row_norms(d_cent.as<float>(), nlist, d, d_cnorm.as<float>(), stream);
     {  // transposed centroids [d][nlist] for the fused coarse kernel
-      std::vector<float> ct((size_t)nlist * d);
+      const int ldc = (nlist + 3) & ~3;  // rows padded to a multiple of 4 (branch-free float4 loads)
+      std::vector<float> ct((size_t)ldc * d, 0.f);
       for (int l = 0; l < nlist; l++)
-        for (int t = 0; t < d; t++) ct[(size_t)t * nlist + l] = centroids[(size_t)l * d + t];
+        for (int t = 0; t < d; t++) ct[(size_t)t * ldc + l] = centroids[(size_t)l * d + t];
       d_centT.ensure(sizeof(float) * ct.size());
       HIPCHECK(hipMemcpyAsync(d_centT.p, ct.data(), sizeof(float) * ct.size(), hipMemcpyHostToDevice, stream));
       HIPCHECK(hipStreamSynchronize(stream));
@@ -453,7 +455,7 @@ struct ivfpq_index {
       if (query_major) {
         launch_scan_topk(a, s);
       } else {
-        const size_t sb = sizeof(uint64_t) * scan_lists_grid() * kStampItems * kStampSlots;
+        const size_t sb = sizeof(uint64_t) * ((size_t)scan_lists_grid() * kStampItems * kStampSlots + (size_t)c * 4);
         if (!stamp_out.empty()) {
           w_stamps.ensure(sb);
           HIPCHECK(hipMemsetAsync(w_stamps.p, 0, sb, s));
@@ -553,6 +555,7 @@ int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivf
     require(d % M == 0, "d must be a multiple of M");
     require(nbits == 8, "only nbits=8 is supported");
     require(scan_supported_M(M), "M=" + std::to_string(M) + " not supported on the GPU (8, 16, 32, 48, 64)");
+    require(d <= 2048, "d > 2048 not supported");
     require(metric == IVFPQ_METRIC_L2 || metric == IVFPQ_METRIC_INNER_PRODUCT, "unknown metric");
     int ndev = 0;
     HIPCHECK(hipGetDeviceCount(&ndev));
@@ -574,6 +577,7 @@ int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivf
     if (so) h->stamp_out = so;
     const char* dbg = std::getenv("IVFPQ_DEBUG");
     h->debug = dbg ? std::atoi(dbg) : 0;
+    if (h->debug & 48) set_coarse_debug((h->debug >> 4) & 3);
     const char* cs = std::getenv("IVFPQ_COARSE");
     h->coarse_fused = !(cs && std::string(cs) == "split");
     const char* sc = std::getenv("IVFPQ_SCAN");

@@ -25,6 +25,7 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
 // the nprobe smallest (dis, list) pairs.  Same arithmetic as launch_l2_dist +
 // launch_select_rows.
 constexpr int kCoarseFusedMax = 8192;
+void set_coarse_debug(int v);  // timing ablations of the fused coarse kernel (wrong results)
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                          int nprobe, float* out_dis, int64_t* out_list, hipStream_t s);
 
@@ -88,6 +89,7 @@ struct ListPlan {
   int32_t* tauq;         // [nq] running k-th distance bound per query (fp32 bits, atomicMin)
   int cap;               // upper bound on the number of work items
   int grid;              // persistent phase-B workgroups (multiple of 8)
+  int seed = 1;          // run the threshold-seed pass (0: every probe in phase B)
 };
 int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
 // phase-B item-count upper bound for a batch (host side, to size ListPlan)

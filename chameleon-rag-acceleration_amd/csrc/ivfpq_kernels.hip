@@ -267,6 +267,87 @@ __device__ __forceinline__ void bulk_merge_row(WaveTopK<1>& tk, float cd, int64_
   tk.refresh_tau();
 }
 
+// ---- selection when every candidate is known up front ------------------------
+// Each lane holds KL (dist, id) entries sorted ascending; the wave emits the k
+// smallest overall (k <= 64) into lanes 0..k-1 with a 64-way merge: per output
+// one butterfly min across lanes (DPP) and a pop on the owning lane.  No
+// per-candidate serial insertion.
+template <int KL>
+__device__ __forceinline__ void cas_asc(float (&d)[KL], int64_t (&id)[KL], int a, int b) {
+  if (lexless(d[b], id[b], d[a], id[a])) {
+    const float td = d[a];
+    const int64_t ti = id[a];
+    d[a] = d[b];
+    id[a] = id[b];
+    d[b] = td;
+    id[b] = ti;
+  }
+}
+
+// in-register bitonic sort of KL (power of two) entries, ascending
+template <int KL>
+__device__ __forceinline__ void lane_sort(float (&d)[KL], int64_t (&id)[KL]) {
+#pragma unroll
+  for (int kk = 2; kk <= KL; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int i = 0; i < KL; i++) {
+        const int pj = i ^ j;
+        if (pj > i) {
+          if ((i & kk) == 0)
+            cas_asc<KL>(d, id, i, pj);
+          else
+            cas_asc<KL>(d, id, pj, i);
+        }
+      }
+    }
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void min_step(float& d, int64_t& id) {
+  const float od = xor_f<J>(d);
+  const int64_t oi = xor_i64<J>(id);
+  if (lexless(od, oi, d, id)) {
+    d = od;
+    id = oi;
+  }
+}
+
+// lanes' lists sorted ascending -> the k smallest into (out_d, out_id) of lanes 0..k-1
+template <int KL>
+__device__ __forceinline__ void wave_kway(float (&d)[KL], int64_t (&id)[KL], int k, int lane, float& out_d,
+                                          int64_t& out_id) {
+  out_d = kInf;
+  out_id = kSentinelId;
+  for (int t = 0; t < k; t++) {
+    float md = d[0];
+    int64_t mi = id[0];
+    min_step<1>(md, mi);
+    min_step<2>(md, mi);
+    min_step<4>(md, mi);
+    min_step<8>(md, mi);
+    min_step<16>(md, mi);
+    min_step<32>(md, mi);
+    // every lane now holds the minimum; the first lane whose head equals it pops
+    const uint64_t own = __ballot(d[0] == md && id[0] == mi);
+    if (lane == __builtin_ctzll(own)) {
+#pragma unroll
+      for (int j = 0; j < KL - 1; j++) {
+        d[j] = d[j + 1];
+        id[j] = id[j + 1];
+      }
+      d[KL - 1] = kInf;
+      id[KL - 1] = kSentinelId;
+    }
+    if (lane == t) {
+      out_d = md;
+      out_id = mi;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ norms
 __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int d,
                                                    float* __restrict__ out) {
@@ -346,6 +427,7 @@ __global__ __launch_bounds__(256) void k_l2_dist(const float* __restrict__ x, co
 // query w's nprobe nearest lists (same rule and arithmetic as k_l2_dist +
 // k_select_rows).
 constexpr int CQ = 4;
+__device__ int g_coarse_debug = 0;  // 1: skip the distance loop, 2: skip the selection (timing only)
 
 template <int R>
 __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
@@ -376,25 +458,29 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
     for (int qq = 0; qq < CQ; qq++)
 #pragma unroll
       for (int u = 0; u < 4; u++) acc[qq][u] = 0.f;
-    if (c4 < nlist) {
-      const bool full = c4 + 4 <= nlist && (nlist & 3) == 0;
-      for (int kk = 0; kk < d; kk++) {
-        float cv[4];
-        if (full) {
-          const float4 v = *reinterpret_cast<const float4*>(centT + (int64_t)kk * nlist + c4);
-          cv[0] = v.x;
-          cv[1] = v.y;
-          cv[2] = v.z;
-          cv[3] = v.w;
-        } else {
+    if (c4 < nlist && !(g_coarse_debug & 1)) {
+      // centT rows are padded to a multiple of 4 columns: branch-free float4 loads
+      const int ldc = (nlist + 3) & ~3;
+      constexpr int KB = 16;  // centroid rows in flight
+      for (int k0 = 0; k0 < d; k0 += KB) {
+        float4 cv[KB];
 #pragma unroll
-          for (int u = 0; u < 4; u++) cv[u] = c4 + u < nlist ? centT[(int64_t)kk * nlist + c4 + u] : 0.f;
+        for (int u = 0; u < KB; u++) {
+          const int kk = min(k0 + u, d - 1);
+          cv[u] = *reinterpret_cast<const float4*>(centT + (int64_t)kk * ldc + c4);
         }
 #pragma unroll
-        for (int qq = 0; qq < CQ; qq++) {
-          const float xv = xs[qq * d + kk];
+        for (int u = 0; u < KB; u++) {
+          if (k0 + u < d) {
 #pragma unroll
-          for (int u = 0; u < 4; u++) acc[qq][u] = __builtin_fmaf(xv, cv[u], acc[qq][u]);
+            for (int qq = 0; qq < CQ; qq++) {
+              const float xv = xs[qq * d + k0 + u];
+              acc[qq][0] = __builtin_fmaf(xv, cv[u].x, acc[qq][0]);
+              acc[qq][1] = __builtin_fmaf(xv, cv[u].y, acc[qq][1]);
+              acc[qq][2] = __builtin_fmaf(xv, cv[u].z, acc[qq][2]);
+              acc[qq][3] = __builtin_fmaf(xv, cv[u].w, acc[qq][3]);
+            }
+          }
         }
       }
     }
@@ -419,6 +505,51 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
   WaveTopK<R> tk;
   tk.init(nprobe);
   const float* drow = dist + wave * nlist;
+  if (g_coarse_debug & 2) {
+    if (lane < nprobe) {
+      out_dis[q * nprobe + lane] = drow[lane];
+      out_list[q * nprobe + lane] = lane;
+    }
+    return;
+  }
+  if constexpr (R == 1) {
+    // 16 candidates per lane per 1024-centroid block: sort in registers, 64-way
+    // merge for the block's nprobe best, fold into the running list
+    float rd = kInf;
+    int64_t ri = kSentinelId;
+    for (int base = 0; base < nlist; base += 1024) {
+      float cd[16];
+      int64_t ci[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int cix = base + u * 64 + lane;
+        cd[u] = cix < nlist ? drow[cix] : kInf;
+        ci[u] = cix < nlist ? (int64_t)cix : kSentinelId;
+      }
+      lane_sort<16>(cd, ci);
+      float bd;
+      int64_t bi;
+      wave_kway<16>(cd, ci, nprobe, lane, bd, bi);
+      if (base == 0) {
+        rd = bd;
+        ri = bi;
+      } else {
+        WaveTopK<1> tk1;
+        tk1.init(nprobe);
+        tk1.d[0] = rd;
+        tk1.id[0] = ri;
+        bulk_merge_row(tk1, bd, bi, lane);
+        rd = tk1.d[0];
+        ri = tk1.id[0];
+      }
+    }
+    if (lane < nprobe) {
+      const bool empty = ri == kSentinelId;
+      out_dis[q * nprobe + lane] = empty ? FLT_MAX : rd;
+      out_list[q * nprobe + lane] = empty ? -1 : ri;
+    }
+    return;
+  }
   for (int base = 0; base < nlist; base += 64) {
     const int cix = base + lane;
     const bool valid = cix < nlist;
@@ -426,12 +557,6 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
     const bool pass = valid && lexless(v, (int64_t)cix, tk.td, tk.ti);
     const uint64_t mask = __ballot(pass);
     if (!mask) continue;
-    if constexpr (R == 1) {
-      if (__popcll(mask) > 6) {
-        bulk_merge_row(tk, pass ? v : kInf, pass ? (int64_t)cix : kSentinelId, lane);
-        continue;
-      }
-    }
     tk.insert(mask, v, (int64_t)cix, lane);
   }
 #pragma unroll
@@ -482,19 +607,50 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
 }
 
 // -------------------------------------------------------------- PQ tables
-// One workgroup per (query, sub-quantizer m): thread j computes T3[q][m][j]
-// (256 = ksub entries, coalesced store); q[m] is read once per workgroup.
+// T3, one workgroup per query: thread t computes entries [16t, 16t+16) of the
+// query's M x 256 table (m = t / 16); q is staged in LDS, codebook rows are
+// contiguous, the 64-B output per thread is stored as 4 x float4.  DSUB = 0 is
+// the generic (runtime dsub) variant.
+template <int DSUB>
 __global__ __launch_bounds__(256) void k_ip_table(const float* __restrict__ x, int64_t n, int d,
                                                   const float* __restrict__ cb, int M, int ksub,
                                                   float* __restrict__ out) {
-  const int64_t q = blockIdx.y;
-  const int m = blockIdx.x;
-  const int j = threadIdx.x;
-  if (j >= ksub) return;
-  const int dsub = d / M;
-  const float* xq = x + q * d + m * dsub;
-  const float* cw = cb + ((int64_t)m * ksub + j) * dsub;
-  out[(q * M + m) * ksub + j] = tree<K_IP>([&](int u) { return xq[u]; }, [&](int u) { return cw[u]; }, dsub);
+  __shared__ float xs[2048];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < d; e += 256) xs[e] = x[q * d + e];
+  __syncthreads();
+  const int dsub = DSUB ? DSUB : d / M;
+  const int total = M * ksub;
+  if constexpr (DSUB > 0) {
+    // 4 entries per round trip: all codebook loads first, then the trees
+    constexpr int EB = 4;
+    for (int e0 = tid; e0 < total; e0 += 256 * EB) {
+      float cw[EB][DSUB];
+#pragma unroll
+      for (int b = 0; b < EB; b++) {
+        const int e = min(e0 + b * 256, total - 1);
+        const float* src = cb + (int64_t)e * DSUB;  // [M][ksub][dsub] == entry-major
+#pragma unroll
+        for (int t = 0; t < DSUB; t++) cw[b][t] = src[t];
+      }
+#pragma unroll
+      for (int b = 0; b < EB; b++) {
+        const int e = e0 + b * 256;
+        if (e < total) {
+          const float* xq = xs + (e / ksub) * DSUB;
+          out[q * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cw[b][t]; }, DSUB);
+        }
+      }
+    }
+  } else {
+    for (int e = tid; e < total; e += 256) {
+      const int m = e / ksub;
+      const float* xq = xs + m * dsub;
+      const float* cwp = cb + (int64_t)e * dsub;
+      out[q * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_precompute_T1(const float* __restrict__ cent, int nlist, int d,
@@ -589,6 +745,11 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
   const int wave = tid >> 6;
   const int64_t q = blockIdx.x;
   const int k = a.k;
+  // diagnostic stamps (seed mode): [q][4] = start, LUT ready, scan done, end
+  auto qstamp = [&](int slot) {
+    if (a.stamps && threadIdx.x == 0) a.stamps[q * 4 + slot] = __builtin_amdgcn_s_memtime();
+  };
+  qstamp(0);
 
   // This thread's slice of the query's T3 (float4 index e*256 + tid).
   float4 t3[NV4];
@@ -602,6 +763,7 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
   tk.init(k);
 
   int p_begin = 0, p_end = a.nprobe;
+  qstamp(2);
   if (a.first_probe) {  // threshold-seed mode: only the first usable probe
     p_begin = a.first_probe[q];
     p_end = min(p_begin + 1, a.nprobe);
@@ -628,37 +790,51 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
     }
     __syncthreads();
 
+    qstamp(1);
     const int64_t beg = a.list_off[l];
     const int64_t n = a.list_off[l + 1] - beg;
     const uint8_t* lc = a.codes + beg * M;
     const int64_t* lid = a.ids + beg;
-    for (int64_t base = wave * 64; base < n; base += 256) {
-      const int64_t i = base + lane;
-      const bool valid = i < n;
-      float dis = d0;
-      if (valid) {
-        CodeWords<M> cw;
-        cw.load(lc + i * M);
+    constexpr int JQ = M <= 16 ? 4 : 2;  // codes per lane per round trip
+    for (int64_t base = wave * 64; base < n; base += 256 * JQ) {
+      CodeWords<M> cw[JQ];
 #pragma unroll
-        for (int m = 0; m < M; m++) dis = dis + lut[m * 256 + cw.byte(m)];
+      for (int j = 0; j < JQ; j++) {
+        const int64_t i = base + j * 256 + lane;
+        cw[j].load(lc + (i < n ? i : 0) * M);  // clamped: branch-free batch of loads
       }
-      const bool maybe = valid && dis <= tk.td;
-      int64_t id = kSentinelId;
-      if constexpr (POSKEY) {
-        id = beg + i;
-      } else {
-        if (maybe) id = lid[i];
-      }
-      const bool pass = maybe && lexless(dis, id, tk.td, tk.ti);
-      const uint64_t mask = __ballot(pass);
-      if (!mask) continue;
-      if constexpr (R == 1) {
-        if (__popcll(mask) > 6) {
-          bulk_merge_row(tk, pass ? dis : kInf, pass ? id : kSentinelId, lane);
-          continue;
+      float dj[JQ];  // m-outer: JQ independent gathers in flight, no branches between
+#pragma unroll
+      for (int j = 0; j < JQ; j++) dj[j] = d0;
+#pragma unroll
+      for (int m = 0; m < M; m++)
+#pragma unroll
+        for (int j = 0; j < JQ; j++) dj[j] = dj[j] + lut[m * 256 + cw[j].byte(m)];
+#pragma unroll
+      for (int j = 0; j < JQ; j++) {
+        const int64_t i = base + j * 256 + lane;
+        const bool valid = i < n;
+        const float dis = dj[j];
+        const bool maybe = valid && dis <= tk.td;
+        int64_t id = kSentinelId;
+        if constexpr (POSKEY) {
+          id = beg + i;
+        } else {
+          if (maybe) id = lid[i];
+        }
+        const bool pass = maybe && lexless(dis, id, tk.td, tk.ti);
+        const uint64_t mask = __ballot(pass);
+        if (mask) {
+          if constexpr (R == 1) {
+            if (__popcll(mask) > 6)
+              bulk_merge_row(tk, pass ? dis : kInf, pass ? id : kSentinelId, lane);
+            else
+              tk.insert(mask, dis, id, lane);
+          } else {
+            tk.insert(mask, dis, id, lane);
+          }
         }
       }
-      tk.insert(mask, dis, id, lane);
     }
   }
 
@@ -676,6 +852,7 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
         a.partI[o + idx] = empty ? -1 : tk.id[r];
       }
     }
+    qstamp(3);
     if (lane == 0 && tk.td < kInf) atomicMin(&a.tauq[q], __float_as_int(tk.td));
     return;
   }
@@ -745,6 +922,10 @@ __global__ __launch_bounds__(256) void k_first_probe(const int64_t* __restrict__
   if (t >= nq) return;
   pl.tauq[t] = __float_as_int(kInf);
   int fp = nprobe;
+  if (!pl.seed) {  // no seed pass: every usable probe goes to phase B
+    pl.first_probe[t] = nprobe;
+    return;
+  }
   for (int p = 0; p < nprobe; p++)
     if (usable_list(lists[t * nprobe + p], lo, hi, list_off)) {
       fp = p;
@@ -857,6 +1038,12 @@ __device__ __forceinline__ void setc(float4& o, int g, float x) {
 // label-sorted, so this equals (distance, label) inside a list.  tau_q is shared
 // across workgroups through global atomicMin (any k real candidates bound the
 // final k-th; a stale read is only a looser bound).
+#ifndef SCAN_VAR
+#define SCAN_VAR 0  // experiment switch: gather order in k_scan_lists
+#endif
+#ifndef SCAN_J16
+#define SCAN_J16 4
+#endif
 constexpr int QCAP = 256;  // per-wave candidate queue entries
 
 template <int M, int G, int R, int J>
@@ -962,6 +1149,46 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
     for (int g = 0; g < G; g++) tk[g].init(k);
     int qn = 0;  // this wave's queue fill (wave-uniform)
 
+    // drain the queue into the per-query top-k lists and publish the bounds
+    auto drain = [&]() {
+      for (int b0 = 0; b0 < qn; b0 += 64) {
+        const int e = b0 + lane;
+        const float cd = e < qn ? qd[wave][e] : kInf;
+        const int ci = e < qn ? qi[wave][e] : 0;
+        const int64_t pos = ci >> 2;
+        const int cg = ci & 3;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          const bool p = e < qn && cg == g && lexless(cd, pos, tk[g].td, tk[g].ti);
+          const uint64_t mk = __ballot(p);
+          if (mk) {
+            if constexpr (R == 1) {
+              if (__popcll(mk) > 6)
+                bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : kSentinelId, lane);
+              else
+                tk[g].insert(mk, cd, pos, lane);
+            } else {
+              tk[g].insert(mk, cd, pos, lane);
+            }
+            bound[g] = fminf(bound[g], tk[g].td);
+          }
+        }
+      }
+      qn = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (g < cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
+      }
+    };
+    auto push = [&](bool pass, uint64_t mask, float dv, int i, int g) {
+      if (pass) {
+        const int sl = qn + __popcll(mask & lanemask_lt);
+        qd[wave][sl] = dv;
+        qi[wave][sl] = (i << 2) | g;
+      }
+      qn += __popcll(mask);
+    };
+
     for (int base = 0; base < n; base += 256 * J) {
       if (base > 0) {
 #pragma unroll
@@ -970,76 +1197,87 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
           cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
         }
       }
-      int jdone = 0;
-      while (jdone < J && base + jdone * 256 < n) {
-        int jstop = J;
+      // all J x G distances first, m-outer: J independent LDS gathers in flight
+      // per step and no control flow between them (per-chain order is the
+      // sequential m order of the oracle)
+      float dis[J][G];
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-          const int i = base + j * 256 + wave * 64 + lane;
-          const bool run = j >= jdone && jstop == J && base + j * 256 < n;  // wave-uniform
-          if (run && qn + 64 * G > QCAP) jstop = j;  // queue could overflow: drain first
-          if (run && jstop == J) {
-            const bool valid = i < n;
-            float dis[G];
+      for (int j = 0; j < J; j++)
 #pragma unroll
-            for (int g = 0; g < G; g++) dis[g] = d0[g];
+        for (int g = 0; g < G; g++) dis[j][g] = d0[g];
+#if SCAN_VAR == 1
 #pragma unroll
-            for (int m = 0; m < M; m++) {
-              const V v = lut[m * 256 + cw[j].byte(m)];
+      for (int j = 0; j < J; j++) {
 #pragma unroll
-              for (int g = 0; g < G; g++) dis[g] = dis[g] + comp(v, g);
-            }
-            if (a.debug & 1) {
+        for (int m = 0; m < M; m++) {
+          const V v = lut[m * 256 + cw[j].byte(m)];
 #pragma unroll
-              for (int g = 0; g < G; g++) asm volatile("" ::"v"(dis[g]));
-            } else {
-#pragma unroll
-              for (int g = 0; g < G; g++) {
-                const bool pass = valid && dis[g] <= bound[g];
-                const uint64_t mask = __ballot(pass);
-                if (pass) {
-                  const int sl = qn + __popcll(mask & lanemask_lt);
-                  qd[wave][sl] = dis[g];
-                  qi[wave][sl] = (i << 2) | g;
-                }
-                qn += __popcll(mask);
-              }
-            }
-          }
+          for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
         }
-        jdone = jstop;
-        if (qn > 0) {  // drain the queue into the per-query top-k lists
-          for (int b0 = 0; b0 < qn; b0 += 64) {
-            const int e = b0 + lane;
-            const float cd = e < qn ? qd[wave][e] : kInf;
-            const int ci = e < qn ? qi[wave][e] : 0;
-            const int64_t pos = ci >> 2;
-            const int cg = ci & 3;
+      }
+#elif SCAN_VAR == 2
 #pragma unroll
-            for (int g = 0; g < G; g++) {
-              const bool p = e < qn && cg == g && lexless(cd, pos, tk[g].td, tk[g].ti);
-              const uint64_t mk = __ballot(p);
-              if (mk) {
-                if constexpr (R == 1) {
-                  if (__popcll(mk) > 6)
-                    bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : kSentinelId, lane);
-                  else
-                    tk[g].insert(mk, cd, pos, lane);
-                } else {
-                  tk[g].insert(mk, cd, pos, lane);
-                }
-                bound[g] = fminf(bound[g], tk[g].td);
-              }
-            }
-          }
-          qn = 0;
+      for (int j0 = 0; j0 < J; j0 += 2) {
 #pragma unroll
-          for (int g = 0; g < G; g++) {
-            if (g < cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
+        for (int m = 0; m < M; m++) {
+#pragma unroll
+          for (int j = j0; j < j0 + 2; j++) {
+            const V v = lut[m * 256 + cw[j].byte(m)];
+#pragma unroll
+            for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
           }
         }
       }
+#else
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+          const V v = lut[m * 256 + cw[j].byte(m)];
+#pragma unroll
+          for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
+        }
+      }
+#endif
+      if (a.debug & 1) {
+#pragma unroll
+        for (int j = 0; j < J; j++)
+#pragma unroll
+          for (int g = 0; g < G; g++) asm volatile("" ::"v"(dis[j][g]));
+        continue;
+      }
+      // push the J chunks' candidates while they fit; otherwise drain (which
+      // also tightens the bounds) and resume.  One drain site keeps code size down.
+      int jj = 0;
+      while (true) {
+        int jstop = J;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+          if (j >= jj && jstop == J) {  // wave-uniform
+            const int i = base + j * 256 + wave * 64 + lane;
+            const bool valid = i < n;
+            uint64_t mk[G];
+            int tj = 0;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              mk[g] = __ballot(valid && dis[j][g] <= bound[g]);
+              tj += __popcll(mk[g]);
+            }
+            if (qn + tj > QCAP) {
+              jstop = j;
+            } else {
+#pragma unroll
+              for (int g = 0; g < G; g++) push((mk[g] >> lane) & 1, mk[g], dis[j][g], i, g);
+            }
+          }
+        }
+        if (jstop == J && qn < QCAP / 2) break;
+        drain();
+        if (jstop == J) break;
+        jj = jstop;
+      }
     }
+    if (qn > 0) drain();
 
     stamp(2, __builtin_amdgcn_s_memtime());
     stamp(4, (uint64_t)n);
@@ -1077,6 +1315,42 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   const int k = a.k;
   const int np = a.nprobe;
   const int fp = pl.first_probe[q];
+  if (R == 1 && k <= 16 && np * 4 <= 64) {
+    // fast path: lane j owns partial list j = (probe j/4, wave j%4), already
+    // sorted by (distance, label); one 64-way merge
+    float d[16];
+    int64_t id[16];
+    const int p = min(lane >> 2, np - 1);
+    bool scanned = false;
+    if ((lane >> 2) < np) {
+      const int64_t l = a.probe_list[q * np + p];
+      scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
+    }
+    const int64_t base = ((q * np + p) * 4 + (lane & 3)) * k;
+    // unconditional, clamped loads (no divergent branch around them)
+    int64_t pos[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      pos[u] = pl.partI[base + min(u, k - 1)];
+      d[u] = pl.partD[base + min(u, k - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const bool ok = scanned && u < k && pos[u] >= 0;
+      const int64_t lab = a.ids[pos[u] >= 0 ? pos[u] : 0];
+      id[u] = ok ? lab : kSentinelId;
+      d[u] = ok ? d[u] : kInf;
+    }
+    float od;
+    int64_t oi;
+    wave_kway<16>(d, id, k, lane, od, oi);
+    if (lane < k) {
+      const bool empty = oi == kSentinelId;
+      a.outD[q * k + lane] = empty ? FLT_MAX : od;
+      a.outI[q * k + lane] = empty ? -1 : oi;
+    }
+    return;
+  }
   WaveTopK<R> tk;
   tk.init(k);
   const int per_probe = 4 * k;
@@ -1200,6 +1474,8 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
   }
 }
 
+void set_coarse_debug(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_coarse_debug), &v, sizeof(int)); }
+
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                          int nprobe, float* out_dis, int64_t* out_list, hipStream_t s) {
   if (nq <= 0) return;
@@ -1227,7 +1503,17 @@ void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, 
 void launch_ip_table(const float* x, int64_t n, int d, const float* cb, int M, int ksub, float* out,
                      hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_ip_table, dim3((unsigned)M, (unsigned)n), dim3(256), 0, s, x, n, d, cb, M, ksub, out);
+  const int dsub = d / M;
+  const dim3 grid((unsigned)n);
+  if (d > 2048 || (M * ksub) % 16 != 0) return;  // guarded by the host (d <= 2048, ksub = 256)
+  switch (dsub) {
+    case 2: hipLaunchKernelGGL(k_ip_table<2>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
+    case 4: hipLaunchKernelGGL(k_ip_table<4>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
+    case 8: hipLaunchKernelGGL(k_ip_table<8>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
+    case 12: hipLaunchKernelGGL(k_ip_table<12>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
+    case 16: hipLaunchKernelGGL(k_ip_table<16>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
+    default: hipLaunchKernelGGL(k_ip_table<0>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
+  }
 }
 
 void launch_precompute_T1(const float* cent, int nlist, int d, const float* cb, int M, int ksub, float* T1,
@@ -1285,13 +1571,14 @@ int list_scan_cap(int64_t nq, int nprobe, int nloc, int G) {
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
   constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 16) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 16) ? 2 : 1;
-  constexpr int J = M <= 8 ? 8 : M <= 16 ? 4 : 2;  // codes per lane per batch (register budget)
+  constexpr int J = M <= 8 ? 8 : M <= 16 ? SCAN_J16 : 2;  // codes per lane per batch (register budget)
   ScanArgs seed = a;
   seed.first_probe = pl.first_probe;
   seed.partD = pl.partD;
   seed.partI = pl.partI;
   seed.tauq = pl.tauq;
-  hipLaunchKernelGGL((k_scan_topk<M, R, true>), dim3((unsigned)a.nq), dim3(256), 0, s, seed);
+  seed.stamps = a.stamps ? a.stamps + (size_t)scan_lists_grid() * kStampItems * kStampSlots : nullptr;
+  if (pl.seed) hipLaunchKernelGGL((k_scan_topk<M, R, true>), dim3((unsigned)a.nq), dim3(256), 0, s, seed);
   hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }

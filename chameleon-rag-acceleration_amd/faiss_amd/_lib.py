@@ -12,7 +12,7 @@ import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_PKG)  # chameleon-rag-acceleration_amd/
-LIB_PATH = os.path.join(ROOT, "lib", "libivfpq.so")
+LIB_PATH = os.environ.get("IVFPQ_LIB") or os.path.join(ROOT, "lib", "libivfpq.so")  # IVFPQ_LIB: A/B builds
 CSRC = os.path.join(ROOT, "csrc")
 
 _lock = threading.Lock()

@@ -3,8 +3,8 @@ import sys
 
 import numpy as np
 
-ITEMS, SLOTS = 32, 6
-a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, ITEMS, SLOTS).astype(np.int64)
+GRID, ITEMS, SLOTS = int(sys.argv[2]) if len(sys.argv) > 2 else 512, 32, 6
+a = np.fromfile(sys.argv[1], dtype=np.uint64)[:GRID * ITEMS * SLOTS].reshape(-1, ITEMS, SLOTS).astype(np.int64)
 valid = a[:, :, 0] > 0
 t0, t1, t2, t3, n, cnt = [a[:, :, i] for i in range(6)]
 load = (t1 - t0)[valid]
