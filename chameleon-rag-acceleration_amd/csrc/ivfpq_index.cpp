@@ -192,11 +192,11 @@ struct ivfpq_index {
   }
 
   // stage timing (HIP events recorded on the launch stream around each stage)
-  enum Stage { ST_COARSE = 0, ST_TABLES = 1, ST_SCAN = 2, ST_N = 3 };
+  enum Stage { ST_COARSE = 0, ST_TABLES = 1, ST_SCAN = 2, ST_LISTS = 3, ST_N = 4 };
   bool timing = false;
   struct Mark {
     int stage;
-    hipEvent_t a, b;
+    hipEvent_t a, b;  // adjacent: &a is passed as an event pair
   };
   std::vector<Mark> marks;
   std::vector<hipEvent_t> ev_pool;
@@ -461,7 +461,9 @@ struct ivfpq_index {
           HIPCHECK(hipMemsetAsync(w_stamps.p, 0, sb, s));
           a.stamps = w_stamps.as<uint64_t>();
         }
-        launch_scan_lists(a, make_plan(c, np, k), s);
+        // ST_LISTS: its two events are re-recorded around the list-scan kernel alone
+        const int tl = mark_begin(ST_LISTS, s);
+        launch_scan_lists(a, make_plan(c, np, k), s, tl >= 0 ? &marks[tl].a : nullptr);
         if (!stamp_out.empty()) {
           std::vector<uint64_t> hs(sb / 8);
           HIPCHECK(hipMemcpyAsync(hs.data(), w_stamps.p, sb, hipMemcpyDeviceToHost, s));

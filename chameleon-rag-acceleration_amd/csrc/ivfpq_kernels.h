@@ -94,7 +94,8 @@ struct ListPlan {
 int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
 // phase-B item-count upper bound for a batch (host side, to size ListPlan)
 int list_scan_cap(int64_t nq, int nprobe, int nloc, int G);
-void launch_scan_lists(const ScanArgs& a, const ListPlan& plan, hipStream_t s);
+// ev_lists (nullable): two events recorded around the phase-B list-scan kernel alone
+void launch_scan_lists(const ScanArgs& a, const ListPlan& plan, hipStream_t s, hipEvent_t* ev_lists = nullptr);
 int scan_lists_grid();  // persistent grid size for the device (2 workgroups per CU)
 
 // merge S sorted partial top-k lists [S][n][k] into [n][k]

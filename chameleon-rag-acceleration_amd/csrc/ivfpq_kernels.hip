@@ -216,12 +216,6 @@ __device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-__device__ __forceinline__ int64_t shfl_xor_i64(int64_t v, int m) {
-  const uint64_t u = (uint64_t)v;
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)u, m, 64);
-  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(u >> 32), m, 64);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 // Merge up to 64 candidates (one per lane; (inf, sentinel) = none) into a
 // single-row top-k: bitonic sort of the candidates, then the classic
@@ -1314,7 +1308,6 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   if (q >= a.nq) return;
   const int k = a.k;
   const int np = a.nprobe;
-  const int fp = pl.first_probe[q];
   if (R == 1 && k <= 16 && np * 4 <= 64) {
     // fast path: lane j owns partial list j = (probe j/4, wave j%4), already
     // sorted by (distance, label); one 64-way merge
@@ -1368,8 +1361,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       if (e < total) {
         const int p = e / per_probe;
         const int64_t l = a.probe_list[q * np + p];
-        const bool scanned = p < np && l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l] &&
-                             (p == fp || fp < np);
+        const bool scanned = p < np && l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
         if (scanned) {
           d[b] = pd[e];
           pos[b] = pi[e];
@@ -1569,7 +1561,7 @@ int list_scan_cap(int64_t nq, int nprobe, int nloc, int G) {
 }
 
 template <int M, int R>
-static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
+static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 16) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 16) ? 2 : 1;
   constexpr int J = M <= 8 ? 8 : M <= 16 ? SCAN_J16 : 2;  // codes per lane per batch (register budget)
   ScanArgs seed = a;
@@ -1579,7 +1571,9 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   seed.tauq = pl.tauq;
   seed.stamps = a.stamps ? a.stamps + (size_t)scan_lists_grid() * kStampItems * kStampSlots : nullptr;
   if (pl.seed) hipLaunchKernelGGL((k_scan_topk<M, R, true>), dim3((unsigned)a.nq), dim3(256), 0, s, seed);
+  if (ev) (void)hipEventRecord(ev[0], s);
   hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+  if (ev) (void)hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
 
@@ -1594,17 +1588,17 @@ int scan_lists_grid() {
 }
 
 template <int M>
-static void launch_lists_M(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
+static void launch_lists_M(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   switch (rows_for(a.k)) {
-    case 1: launch_lists_MR<M, 1>(a, pl, s); break;
-    case 2: launch_lists_MR<M, 2>(a, pl, s); break;
-    case 4: launch_lists_MR<M, 4>(a, pl, s); break;
-    case 8: launch_lists_MR<M, 8>(a, pl, s); break;
-    default: launch_lists_MR<M, 16>(a, pl, s); break;
+    case 1: launch_lists_MR<M, 1>(a, pl, s, ev); break;
+    case 2: launch_lists_MR<M, 2>(a, pl, s, ev); break;
+    case 4: launch_lists_MR<M, 4>(a, pl, s, ev); break;
+    case 8: launch_lists_MR<M, 8>(a, pl, s, ev); break;
+    default: launch_lists_MR<M, 16>(a, pl, s, ev); break;
   }
 }
 
-void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
+void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev_lists) {
   if (a.nq <= 0) return;
   const int G = list_scan_group(a.M, a.k);
   const int64_t npairs = a.nq * a.nprobe;
@@ -1617,11 +1611,11 @@ void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s) {
   hipLaunchKernelGGL(k_bucket_scatter, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.probe_dis0,
                      a.nq, a.nprobe, a.list_lo, G, pl);
   switch (a.M) {
-    case 8: launch_lists_M<8>(a, pl, s); break;
-    case 16: launch_lists_M<16>(a, pl, s); break;
-    case 32: launch_lists_M<32>(a, pl, s); break;
-    case 48: launch_lists_M<48>(a, pl, s); break;
-    case 64: launch_lists_M<64>(a, pl, s); break;
+    case 8: launch_lists_M<8>(a, pl, s, ev_lists); break;
+    case 16: launch_lists_M<16>(a, pl, s, ev_lists); break;
+    case 32: launch_lists_M<32>(a, pl, s, ev_lists); break;
+    case 48: launch_lists_M<48>(a, pl, s, ev_lists); break;
+    case 64: launch_lists_M<64>(a, pl, s, ev_lists); break;
     default: break;
   }
 }

@@ -365,15 +365,15 @@ class IndexIVFPQ:
         return D, I
 
     # ------------------------------------------------------------ stage timing
-    STAGES = ("coarse", "tables", "scan")
+    STAGES = ("coarse", "tables", "scan", "lists")
 
     def set_timing(self, on=True):
         _lib.check(_lib.load().ivfpq_set_timing(self._h, 1 if on else 0))
 
     def get_timing(self):
         """{stage: (total_ms, launches)} since the last call (waits for the events)."""
-        ms = (ctypes.c_double * 3)()
-        cnt = (ctypes.c_int64 * 3)()
+        ms = (ctypes.c_double * len(self.STAGES))()
+        cnt = (ctypes.c_int64 * len(self.STAGES))()
         _lib.check(_lib.load().ivfpq_get_timing(self._h, ms, cnt))
         return {s: (ms[i], cnt[i]) for i, s in enumerate(self.STAGES)}
 

@@ -60,6 +60,25 @@ def test_search_matches_golden(golden_dir, case):
     assert_same(D, I, z["or_D"], z["or_I"])
 
 
+@pytest.mark.parametrize("scan", ["query", "seedless"])
+@pytest.mark.parametrize("case", CASES)
+def test_alternative_scan_paths_match_golden(golden_dir, case, scan, monkeypatch):
+    """The query-major fused kernel (IVFPQ_SCAN=query) and the list-major path
+    without the threshold-seed pass (IVFPQ_DEBUG=64) give the same results as
+    the default path.  Both switches are read when the index is created."""
+    z = load_case(golden_dir, case)
+    if scan == "query":
+        monkeypatch.setenv("IVFPQ_SCAN", "query")
+    else:
+        monkeypatch.setenv("IVFPQ_DEBUG", "64")
+    ix = gpu_index(z)
+    for k in (int(z["k"]), 100):
+        ox = oracle_index(z)
+        Dr, Ir = ox.search(z["xq"], k)
+        D, I = ix.search(z["xq"], k)
+        assert_same(D, I, Dr, Ir)
+
+
 @pytest.mark.parametrize("case", CASES)
 def test_coarse_and_tables_match_oracle(golden_dir, case):
     import torch
