@@ -160,7 +160,7 @@ struct ivfpq_index {
   DevBuf p_first, p_slot, p_cnt, p_boff, p_it1, p_nit, p_D, p_I, p_tau;
   bool query_major = false;
   bool sys_scan = true;  // M = 16: k_scan_sys (IVFPQ_SCAN=lists selects k_scan_lists, A/B)
-  bool t3_inkernel = true;  // k_scan_sys forms T3 from the codebook when d = 128 (IVFPQ_T3=mem: from the T3 buffer)
+  bool t3_inkernel = false;  // k_scan_sys forms T3 from the codebook when d = 128 (IVFPQ_T3=reg; default: T3 buffer)
   int debug = 0;  // IVFPQ_DEBUG: kernel timing ablations (wrong results)
   std::string stamp_out;  // IVFPQ_STAMPS=<path>: dump phase-B in-kernel stamps (diagnostic)
   DevBuf w_stamps;  // IVFPQ_SCAN=query selects the query-major kernel (A/B only)
@@ -627,7 +627,7 @@ int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivf
     h->query_major = sc && std::string(sc) == "query";
     h->sys_scan = !(sc && std::string(sc) == "lists");
     const char* t3 = std::getenv("IVFPQ_T3");
-    h->t3_inkernel = !(t3 && std::string(t3) == "mem");
+    h->t3_inkernel = t3 && std::string(t3) == "reg";
     h->init_stream();
     *out = h.release();
   });

@@ -1368,6 +1368,7 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
 // of query plus VALU work.
 constexpr int SYS_M = 16;
 constexpr int SYS_G = 4;
+constexpr int SYS_PF = 4;  // code-chunk prefetch depth (super-steps)
 
 __device__ __forceinline__ float shr1z(float v) {
   // row_shr:1 with bound_ctrl: lane 0 of each row reads 0
@@ -1492,7 +1493,10 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
     }
     const int cend = min(rb1 * 16, n);
     const uint8_t* col = a.scodes + soff * 256 + mm * 16;
-    uint4 nxt = *reinterpret_cast<const uint4*>(col + (int64_t)rb0 * 256);
+    // code chunks are loaded SYS_PF super-steps ahead of their use (the first ones land during the LUT build)
+    uint4 cq[SYS_PF];
+#pragma unroll
+    for (int p = 0; p < SYS_PF; p++) cq[p] = *reinterpret_cast<const uint4*>(col + (int64_t)min(rb0 + p, nc) * 256);
 
     __syncthreads();  // the previous item is done with the LDS
 #pragma unroll
@@ -1567,17 +1571,30 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
 #pragma unroll
     for (int g = 0; g < G; g++) P[g] = __builtin_nanf("");
 
-    // 16 steps of one super-step; CHECKED masks completions at or past cend
+    // 16 steps of one super-step; CHECKED masks completions at or past cend.
+    // The LDS lookups of SB steps are issued before any of them is consumed:
+    // the candidate pushes store to LDS, so reads written after them in program
+    // order would each wait out the full LDS latency.
+    constexpr int SB = CBREG ? 8 : 16;
     auto steps = [&](const uint4 cur, const int cb, auto checked_tag) {
       constexpr bool CHECKED = decltype(checked_tag)::value;
       const int lim = cend - cb;  // the completion of step t is code cb + t: valid iff t < lim
 #pragma unroll
-      for (int t = 0; t < 16; t++) {
-        const uint32_t w = t < 4 ? cur.x : t < 8 ? cur.y : t < 12 ? cur.z : cur.w;
-        // (byte t of w) << 8 | m << 4 in one v_perm: {b0: mbase.b0, b1: w.b(t&3), b2, b3: 0}
-        const uint32_t sel = 0x0c0c0000u | ((uint32_t)(4 + (t & 3)) << 8);
-        const uint32_t addr = __builtin_amdgcn_perm(w, mbase, sel);
-        const float4 lv = *reinterpret_cast<const float4*>(lut + addr);
+      for (int t0 = 0; t0 < 16; t0 += SB) {
+        float4 lvb[SB];
+#pragma unroll
+        for (int u = 0; u < SB; u++) {
+          const int t = t0 + u;
+          const uint32_t w = t < 4 ? cur.x : t < 8 ? cur.y : t < 12 ? cur.z : cur.w;
+          // (byte t of w) << 8 | m << 4 in one v_perm: {b0: mbase.b0, b1: w.b(t&3), b2, b3: 0}
+          const uint32_t sel = 0x0c0c0000u | ((uint32_t)(4 + (t & 3)) << 8);
+          const uint32_t addr = __builtin_amdgcn_perm(w, mbase, sel);
+          lvb[u] = *reinterpret_cast<const float4*>(lut + addr);
+        }
+#pragma unroll
+      for (int u = 0; u < SB; u++) {
+        const int t = t0 + u;
+        const float4 lv = lvb[u];
         P[0] = shr1z(P[0]) + lv.x;
         P[1] = shr1z(P[1]) + lv.y;
         P[2] = shr1z(P[2]) + lv.z;
@@ -1605,11 +1622,14 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
           }
         }
       }
+      }
     };
 
     for (int i = 0; i <= dmax; i++) {
-      const uint4 cur = nxt;
-      nxt = *reinterpret_cast<const uint4*>(col + (int64_t)min(rb0 + i + 1, nc) * 256);
+      const uint4 cur = cq[0];
+#pragma unroll
+      for (int p = 0; p + 1 < SYS_PF; p++) cq[p] = cq[p + 1];
+      cq[SYS_PF - 1] = *reinterpret_cast<const uint4*>(col + (int64_t)min(rb0 + i + SYS_PF, nc) * 256);
       if (qn > 0) drain();  // a super-step pushes at most 16 steps x 4 rows x 4 queries = QCAP entries
       const int cb = 16 * (rb0 + i) - 15;
       if (i < dmin)

@@ -60,18 +60,18 @@ def test_search_matches_golden(golden_dir, case):
     assert_same(D, I, z["or_D"], z["or_I"])
 
 
-@pytest.mark.parametrize("scan", ["query", "seedless", "lists", "t3mem", "globalq"])
+@pytest.mark.parametrize("scan", ["query", "seedless", "lists", "t3reg", "globalq"])
 @pytest.mark.parametrize("case", CASES)
 def test_alternative_scan_paths_match_golden(golden_dir, case, scan, monkeypatch):
     """Every scan path gives the oracle's result: the query-major fused kernel
     (IVFPQ_SCAN=query), list-major without seed items first (IVFPQ_DEBUG=64),
     the interleaved-LUT k_scan_lists instead of the systolic k_scan_sys for M=16
-    (IVFPQ_SCAN=lists), k_scan_sys reading T3 from memory instead of forming it
-    from the codebook (IVFPQ_T3=mem), and one global work queue (IVFPQ_DEBUG=8).
+    (IVFPQ_SCAN=lists), k_scan_sys forming T3 from the codebook instead of reading
+    the T3 buffer (IVFPQ_T3=reg), and one global work queue (IVFPQ_DEBUG=8).
     The switches are read when the index is created."""
     z = load_case(golden_dir, case)
     env = {"query": ("IVFPQ_SCAN", "query"), "seedless": ("IVFPQ_DEBUG", "64"), "lists": ("IVFPQ_SCAN", "lists"),
-           "t3mem": ("IVFPQ_T3", "mem"), "globalq": ("IVFPQ_DEBUG", "8")}[scan]
+           "t3reg": ("IVFPQ_T3", "reg"), "globalq": ("IVFPQ_DEBUG", "8")}[scan]
     monkeypatch.setenv(*env)
     ix = gpu_index(z)
     for k in (int(z["k"]), 100):
