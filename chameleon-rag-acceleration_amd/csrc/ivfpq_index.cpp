@@ -184,7 +184,7 @@ struct ivfpq_index {
     p_cnt.ensure(sizeof(int32_t) * std::max(2 * nloc, 1));
     p_boff.ensure(sizeof(int32_t) * std::max(2 * nloc, 1));
     p_it1.ensure(sizeof(int32_t) * 16 * pl.cap);
-    p_nit.ensure(sizeof(int32_t) * 16);
+    p_nit.ensure(sizeof(int32_t) * 32);
     p_D.ensure(sizeof(float) * nq * np * 4 * k);
     p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
     p_tau.ensure(sizeof(int32_t) * nq);

@@ -90,7 +90,8 @@ struct ListPlan {
   int32_t* cnt;          // [2 * nloc]  per key: seed keys [0, nloc), other keys [nloc, 2 nloc)
   int32_t* ioff;         // [2 * nloc]  first work item of each key
   int32_t* recs;         // [cap][16] item: list, count, size, offset(2), pairs(4), dis0(4), scode chunk offset(2)
-  int32_t* n_items;      // [16]: [0] items, [1..8] per-XCD-group work counters, [9] seed items
+  int32_t* n_items;      // [32]: [0] items, [9] seed items, [1..8] / [17..24] per-XCD-group work counters
+                         // of the seed / other-items launches
   float* partD;          // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k
   int64_t* partI;        // same shape: global code positions (-1 = none)
   int32_t* tauq;         // [nq] running k-th distance bound per query (fp32 bits, atomicMin)
@@ -100,6 +101,7 @@ struct ListPlan {
   int seed = 1;          // order seed items first (0: one undifferentiated key per list)
   int sys = 0;           // M = 16: systolic conflict-free scan (k_scan_sys); 0: k_scan_lists
   int cbreg = 0;         // k_scan_sys forms T3 in-kernel from the codebook (d = 128, M = 16)
+  int phase = 0;         // items of one scan launch: 0 all, 1 seed items, 2 the rest (set per launch)
 };
 int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
 bool sys_scan_supported(int M, int k);  // k_scan_sys serves this (M, k)

@@ -989,12 +989,18 @@ __global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, c
   }
   if (tid == PLAN_T - 1) pl.n_items[0] = part[PLAN_T - 1];
   if (tid == 0 && nloc == 0) pl.n_items[9] = 0;
-  if (tid < 8) pl.n_items[1 + tid] = 0;  // per-XCD-group work counters of the scan
+  if (tid < 8) {  // per-XCD-group work counters of the scan launches
+    pl.n_items[1 + tid] = 0;
+    pl.n_items[17 + tid] = 0;
+  }
 }
 
 // This workgroup's items: its XCD group's share of the seed items [0, S), then
 // its share of the rest [S, N); contiguous shares keep the consecutive items of
 // one list (same T1 row, same codes) on one XCD's L2.  global_q: one queue.
+// pl.phase selects the items of this launch: 0 = all (seed items first), 1 = seed
+// items only, 2 = the rest only (a separate seed launch makes every bound tau_q
+// final before the bulk of the items start).
 struct ItemRange {
   int s0, ns, r0, nr;
   __device__ __forceinline__ int item(int v) const { return v < ns ? s0 + v : r0 + (v - ns); }
@@ -1002,20 +1008,26 @@ struct ItemRange {
 };
 __device__ __forceinline__ ItemRange item_range(const ListPlan& pl, bool global_q, int grp) {
   const int N = pl.n_items[0], S = pl.n_items[9];
+  const int a0 = pl.phase == 2 ? S : 0, a1 = pl.phase == 1 ? S : N;  // items of this launch
+  const int S1 = min(max(S, a0), a1);                                 // seed items end here
   ItemRange r;
   if (global_q) {
-    r.s0 = 0;
-    r.ns = N;
-    r.r0 = N;
+    r.s0 = a0;
+    r.ns = a1 - a0;
+    r.r0 = a1;
     r.nr = 0;
     return r;
   }
-  const int ps = (S + 7) >> 3, pr = (N - S + 7) >> 3;
-  r.s0 = grp * ps;
-  r.ns = max(0, min(S, r.s0 + ps) - r.s0);
-  r.r0 = S + grp * pr;
-  r.nr = max(0, min(N, r.r0 + pr) - r.r0);
+  const int ps = (S1 - a0 + 7) >> 3, pr = (a1 - S1 + 7) >> 3;
+  r.s0 = a0 + grp * ps;
+  r.ns = max(0, min(S1, r.s0 + ps) - r.s0);
+  r.r0 = S1 + grp * pr;
+  r.nr = max(0, min(a1, r.r0 + pr) - r.r0);
   return r;
+}
+// per-launch work counters: n_items[1..8] (phase 0/1), n_items[17..24] (phase 2)
+__device__ __forceinline__ int* work_counter(const ListPlan& pl, int grp) {
+  return pl.n_items + (pl.phase == 2 ? 17 : 1) + grp;
 }
 
 // scatter each phase-B pair id into its work item record
@@ -1111,7 +1123,7 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
   };
   // dynamic work fetching inside the XCD group (items vary from 1 to ~3k codes)
   __shared__ int s_next;
-  int* ctr = pl.n_items + 1 + grp;
+  int* ctr = work_counter(pl, grp);
   if (tid == 0) s_next = atomicAdd(ctr, 1);
   __syncthreads();
   for (int v = s_next; v < rng.count(); v = s_next, it_no++) {
@@ -1394,6 +1406,7 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
   __shared__ __attribute__((aligned(16))) unsigned char lut[LUT_BYTES];
   __shared__ float qd[4][QCAP];
   __shared__ int32_t qi[4][QCAP];  // (code position in list << 2) | g
+  __shared__ float wkth[4][SYS_G];  // each wave's current k-th distance per query: shared admission bound
   __shared__ int s_next;
 
   const int tid = threadIdx.x;
@@ -1429,7 +1442,7 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
     if (a.stamps && tid == 0 && it_no < kStampItems)
       a.stamps[((int64_t)blockIdx.x * kStampItems + it_no) * kStampSlots + slot] = v;
   };
-  int* ctr = pl.n_items + 1 + grp;
+  int* ctr = work_counter(pl, grp);
   if (tid == 0) s_next = atomicAdd(ctr, 1);
   __syncthreads();
   for (int v = s_next; v < rng.count(); v = s_next, it_no++) {
@@ -1499,6 +1512,7 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
     for (int p = 0; p < SYS_PF; p++) cq[p] = *reinterpret_cast<const uint4*>(col + (int64_t)min(rb0 + p, nc) * 256);
 
     __syncthreads();  // the previous item is done with the LDS
+    if (tid < 4 * G) wkth[tid / G][tid % G] = kInf;
 #pragma unroll
     for (int it = 0; it < 4; it++) {
       const int jq = (tid >> 4) + 16 * it;
@@ -1559,9 +1573,21 @@ __global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
         }
       }
       qn = 0;
+      // tighten the bounds with what the other waves (LDS) and workgroups (tau_q)
+      // have found: any k real candidates bound the final k-th distance
 #pragma unroll
       for (int g = 0; g < G; g++) {
-        if (g < cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
+        if (g < cnt && tk[g].td < kInf && lane == 0) {
+          atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
+          wkth[wave][g] = tk[g].td;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (g < cnt) {
+          const float wb = fminf(fminf(wkth[0][g], wkth[1][g]), fminf(wkth[2][g], wkth[3][g]));
+          bound[g] = fminf(bound[g], fminf(wb, __int_as_float(pl.tauq[qix[g]])));
+        }
       }
       set_bv();
     };
@@ -1933,17 +1959,22 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 16) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 16) ? 2 : 1;
   constexpr int J = M <= 8 ? 8 : M <= 16 ? SCAN_J16 : 2;  // codes per lane per batch (register budget)
   if (ev) (void)hipEventRecord(ev[0], s);
-  bool done = false;
-  if constexpr (M == SYS_M && R * SYS_G <= 16) {
-    if (pl.sys) {
-      if (pl.cbreg)
-        hipLaunchKernelGGL((k_scan_sys<R, true>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
-      else
-        hipLaunchKernelGGL((k_scan_sys<R, false>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
-      done = true;
+  // seed items in a launch of their own, then the rest (pl.seed == 0: one launch)
+  for (int ph = pl.seed ? 1 : 0; ph <= (pl.seed ? 2 : 0); ph++) {
+    ListPlan p = pl;
+    p.phase = ph;
+    bool done = false;
+    if constexpr (M == SYS_M && R * SYS_G <= 16) {
+      if (p.sys) {
+        if (p.cbreg)
+          hipLaunchKernelGGL((k_scan_sys<R, true>), dim3((unsigned)p.grid), dim3(256), 0, s, a, p);
+        else
+          hipLaunchKernelGGL((k_scan_sys<R, false>), dim3((unsigned)p.grid), dim3(256), 0, s, a, p);
+        done = true;
+      }
     }
+    if (!done) hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)p.grid), dim3(256), 0, s, a, p);
   }
-  if (!done) hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   if (ev) (void)hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
