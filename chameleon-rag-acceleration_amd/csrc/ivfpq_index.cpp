@@ -151,7 +151,6 @@ struct ivfpq_index {
   int64_t next_id = 0;
 
   DevBuf d_cent, d_centT, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off;
-  DevBuf d_scodes, d_soff;  // M = 16: systolic code image + per-list chunk offsets (k_scan_sys)
   bool dirty = true;
   hipStream_t stream = nullptr;
   // scratch
@@ -159,32 +158,24 @@ struct ivfpq_index {
   // list-major scan plan workspaces
   DevBuf p_first, p_slot, p_cnt, p_boff, p_it1, p_nit, p_D, p_I, p_tau;
   bool query_major = false;
-  bool sys_scan = true;  // M = 16: k_scan_sys (IVFPQ_SCAN=lists selects k_scan_lists, A/B)
-  bool t3_inkernel = false;  // k_scan_sys forms T3 from the codebook when d = 128 (IVFPQ_T3=reg; default: T3 buffer)
   int debug = 0;  // IVFPQ_DEBUG: kernel timing ablations (wrong results)
   std::string stamp_out;  // IVFPQ_STAMPS=<path>: dump phase-B in-kernel stamps (diagnostic)
   DevBuf w_stamps;  // IVFPQ_SCAN=query selects the query-major kernel (A/B only)
   std::mutex mu;
 
-  bool use_sys(int k) const { return sys_scan && sys_scan_supported(M, k); }
-  bool use_cbreg(int k) const { return use_sys(k) && t3_inkernel && d == 128; }
-
   ListPlan make_plan(int64_t nq, int np, int k) {
     const int nloc = list_hi - list_lo;
+    const int G = list_scan_group(M, k);
     ListPlan pl;
-    pl.sys = use_sys(k) ? 1 : 0;
-    pl.cbreg = use_cbreg(k) ? 1 : 0;
-    pl.soff = pl.sys ? d_soff.as<int64_t>() : nullptr;
-    const int G = pl.sys ? 4 : list_scan_group(M, k);
     pl.cap = list_scan_cap(nq, np, nloc, G);
     pl.grid = scan_lists_grid();
     pl.seed = (debug & 64) ? 0 : 1;
     p_first.ensure(sizeof(int32_t) * nq);
     p_slot.ensure(sizeof(int32_t) * nq * np);
-    p_cnt.ensure(sizeof(int32_t) * std::max(2 * nloc, 1));
-    p_boff.ensure(sizeof(int32_t) * std::max(2 * nloc, 1));
+    p_cnt.ensure(sizeof(int32_t) * std::max(nloc, 1));
+    p_boff.ensure(sizeof(int32_t) * std::max(nloc, 1));
     p_it1.ensure(sizeof(int32_t) * 16 * pl.cap);
-    p_nit.ensure(sizeof(int32_t) * 32);
+    p_nit.ensure(sizeof(int32_t) * 16);
     p_D.ensure(sizeof(float) * nq * np * 4 * k);
     p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
     p_tau.ensure(sizeof(int32_t) * nq);
@@ -369,32 +360,6 @@ struct ivfpq_index {
       HIPCHECK(hipMemcpyAsync(d_ids.p, ids.data(), sizeof(int64_t) * ids.size(), hipMemcpyHostToDevice, stream));
     }
     HIPCHECK(hipMemcpyAsync(d_off.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, stream));
-    std::vector<uint8_t> sc;
-    if (M == 16) {
-      // Systolic image for k_scan_sys (ivfpq_kernels.hip): per list ceil(n/16) + 1
-      // chunks of 256 B; chunk b, lane m, byte t = byte m of code 16 b + t - m.
-      std::vector<int64_t> so(nlist + 1, 0);
-      for (int l = 0; l < nlist; l++) {
-        const int64_t n = off[l + 1] - off[l];
-        so[l + 1] = so[l] + (n ? (n + 15) / 16 + 1 : 0);
-      }
-      sc.assign((size_t)so[nlist] * 256, 0);
-      for (int l = 0; l < nlist; l++) {
-        const int64_t n = off[l + 1] - off[l];
-        const uint8_t* lc = codes.data() + off[l] * 16;
-        uint8_t* dst = sc.data() + so[l] * 256;
-        for (int64_t b = 0; b < so[l + 1] - so[l]; b++)
-          for (int m = 0; m < 16; m++)
-            for (int t = 0; t < 16; t++) {
-              const int64_t c = 16 * b + t - m;
-              if (c >= 0 && c < n) dst[b * 256 + m * 16 + t] = lc[c * 16 + m];
-            }
-      }
-      d_scodes.ensure(std::max<size_t>(256, sc.size()));
-      d_soff.ensure(sizeof(int64_t) * so.size());
-      if (!sc.empty()) HIPCHECK(hipMemcpyAsync(d_scodes.p, sc.data(), sc.size(), hipMemcpyHostToDevice, stream));
-      HIPCHECK(hipMemcpyAsync(d_soff.p, so.data(), sizeof(int64_t) * so.size(), hipMemcpyHostToDevice, stream));
-    }
     HIPCHECK(hipStreamSynchronize(stream));
     dirty = false;
   }
@@ -466,18 +431,12 @@ struct ivfpq_index {
         lists = w_lists.as<int64_t>();
         dis0 = w_dis0.as<float>();
       }
-      const bool cbreg = !query_major && use_cbreg(k);
-      if (!cbreg) {  // the in-kernel LUT build of k_scan_sys<CBREG> needs no T3 buffer
-        const int tt = mark_begin(ST_TABLES, s);
-        launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
-        mark_end(tt, s);
-      }
+      const int tt = mark_begin(ST_TABLES, s);
+      launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
+      mark_end(tt, s);
       ScanArgs a;
       a.T1 = d_T1.as<float>();
       a.T3 = w_T3.as<float>();
-      a.xq = xq;
-      a.cb = d_cb.as<float>();
-      a.scodes = M == 16 ? d_scodes.as<uint8_t>() : nullptr;
       a.codes = d_codes.as<uint8_t>();
       a.ids = d_ids.as<int64_t>();
       a.list_off = d_off.as<int64_t>();
@@ -625,9 +584,6 @@ int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivf
     h->coarse_fused = !(cs && std::string(cs) == "split");
     const char* sc = std::getenv("IVFPQ_SCAN");
     h->query_major = sc && std::string(sc) == "query";
-    h->sys_scan = !(sc && std::string(sc) == "lists");
-    const char* t3 = std::getenv("IVFPQ_T3");
-    h->t3_inkernel = t3 && std::string(t3) == "reg";
     h->init_stream();
     *out = h.release();
   });

@@ -46,10 +46,6 @@ struct ScanArgs {
   const float* T1;          // [nlist][M][ksub]
   const float* T3;          // [nq][M][ksub]
   const uint8_t* codes;     // [n_codes][M], lists concatenated
-  // M = 16 systolic image (k_scan_sys): per list ceil(n/16)+1 chunks of 256 B, see upload_lists
-  const uint8_t* scodes = nullptr;
-  const float* xq = nullptr;  // [nq][d] queries (k_scan_sys builds T3 from these and the codebook)
-  const float* cb = nullptr;  // [M][256][dsub] codebook
   const int64_t* ids;       // [n_codes]
   const int64_t* list_off;  // [nlist + 1]
   const int64_t* probe_list;  // [nq][nprobe]
@@ -76,35 +72,26 @@ constexpr int kStampSlots = 6;   // per item: start, LUT ready, scan done, merge
 void launch_scan_topk(const ScanArgs& a, hipStream_t s);
 bool scan_supported_M(int M);
 
-// ---- List-major scan ----------------------------------------
-// Work item = (inverted list, up to G queries probing it).  Items are bucketed
-// under two keys per list: "seed" pairs (each query's first usable probe, its
-// nearest list) come first, then every other pair.  Each persistent workgroup
-// takes its XCD group's share of the seed items before its share of the rest,
-// so the per-query bound tau_q (k-th distance seen so far, global atomicMin)
-// is tight by the time most items run; admission is dis <= min(tau_q, own k-th).
-// A per-query merge combines the partials.
+// ---- Two-phase scan ------------------------------------------
+// Phase A (query-major k_scan_topk in seed mode): each query's first usable
+// probe, giving a per-query bound tau_q = its k-th distance.  Phase B
+// (list-major): work item = (inverted list, up to G queries probing it), every
+// other probe, admission dis <= tau_q.  A per-query merge combines the partials.
 struct ListPlan {
-  int32_t* first_probe;  // [nq]  first usable probe (nprobe: none, or seed keys off)
+  int32_t* first_probe;  // [nq]
   int32_t* slot;         // [nq * nprobe]
-  int32_t* cnt;          // [2 * nloc]  per key: seed keys [0, nloc), other keys [nloc, 2 nloc)
-  int32_t* ioff;         // [2 * nloc]  first work item of each key
-  int32_t* recs;         // [cap][16] item: list, count, size, offset(2), pairs(4), dis0(4), scode chunk offset(2)
-  int32_t* n_items;      // [32]: [0] items, [9] seed items, [1..8] / [17..24] per-XCD-group work counters
-                         // of the seed / other-items launches
+  int32_t* cnt;          // [nloc]
+  int32_t* ioff;         // [nloc]  first work item of each list
+  int32_t* recs;         // [cap][16] work item: list, count, size, offset(2), pairs(4), coarse dist(4)
+  int32_t* n_items;      // [1]
   float* partD;          // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k
   int64_t* partI;        // same shape: global code positions (-1 = none)
   int32_t* tauq;         // [nq] running k-th distance bound per query (fp32 bits, atomicMin)
-  const int64_t* soff = nullptr;  // [nlist] chunk offset of each list in ScanArgs::scodes (k_scan_sys)
   int cap;               // upper bound on the number of work items
-  int grid;              // persistent workgroups (multiple of 8)
-  int seed = 1;          // order seed items first (0: one undifferentiated key per list)
-  int sys = 0;           // M = 16: systolic conflict-free scan (k_scan_sys); 0: k_scan_lists
-  int cbreg = 0;         // k_scan_sys forms T3 in-kernel from the codebook (d = 128, M = 16)
-  int phase = 0;         // items of one scan launch: 0 all, 1 seed items, 2 the rest (set per launch)
+  int grid;              // persistent phase-B workgroups (multiple of 8)
+  int seed = 1;          // run the threshold-seed pass (0: every probe in phase B)
 };
 int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
-bool sys_scan_supported(int M, int k);  // k_scan_sys serves this (M, k)
 // phase-B item-count upper bound for a batch (host side, to size ListPlan)
 int list_scan_cap(int64_t nq, int nprobe, int nloc, int G);
 // ev_lists (nullable): two events recorded around the phase-B list-scan kernel alone

@@ -24,7 +24,6 @@
 #include <stdint.h>
 
 #include <algorithm>
-#include <type_traits>
 
 #include <hip/hip_runtime.h>
 
@@ -908,23 +907,16 @@ __device__ __forceinline__ bool usable_list(int64_t l, int lo, int hi, const int
   return l >= lo && l < hi && list_off[l + 1] > list_off[l];
 }
 
-// bucket of pair i (list l in [lo, hi)): the seed key of l if p is the query's
-// first usable probe, else l's second key
-__device__ __forceinline__ int bucket_key(int64_t i, int64_t l, int nprobe, int lo, int hi, const ListPlan& pl) {
-  const int j = (int)(l - lo);
-  return (int)(i % nprobe) == pl.first_probe[i / nprobe] ? j : (hi - lo) + j;
-}
-
-// first usable probe per query (nprobe if none); also zeroes the per-key counters
+// first usable probe per query (nprobe if none); also zeroes the per-list counters
 __global__ __launch_bounds__(256) void k_first_probe(const int64_t* __restrict__ lists, int64_t nq, int nprobe,
                                                      const int64_t* __restrict__ list_off, int lo, int hi,
                                                      ListPlan pl) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t < 2 * (int64_t)(hi - lo)) pl.cnt[t] = 0;
+  if (t < (int64_t)(hi - lo)) pl.cnt[t] = 0;
   if (t >= nq) return;
   pl.tauq[t] = __float_as_int(kInf);
   int fp = nprobe;
-  if (!pl.seed) {  // no seed keys: every usable probe under the list's second key
+  if (!pl.seed) {  // no seed pass: every usable probe goes to phase B
     pl.first_probe[t] = nprobe;
     return;
   }
@@ -943,7 +935,8 @@ __global__ __launch_bounds__(256) void k_bucket_count(const int64_t* __restrict_
   if (i >= nq * nprobe) return;
   const int64_t l = lists[i];
   int s = -1;
-  if (usable_list(l, lo, hi, list_off)) s = atomicAdd(&pl.cnt[bucket_key(i, l, nprobe, lo, hi, pl)], 1);
+  if (usable_list(l, lo, hi, list_off) && (int)(i % nprobe) != pl.first_probe[i / nprobe])
+    s = atomicAdd(&pl.cnt[(int)(l - lo)], 1);
   pl.slot[i] = s;
 }
 
@@ -952,9 +945,8 @@ __global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, c
   __shared__ int32_t part[PLAN_T];
   const int tid = threadIdx.x;
   const int nloc = hi - lo;
-  const int nkeys = 2 * nloc;  // seed keys, then the other keys: records come out seed items first
-  const int chunk = (nkeys + PLAN_T - 1) / PLAN_T;
-  const int j0 = min(nkeys, tid * chunk), j1 = min(nkeys, j0 + chunk);
+  const int chunk = (nloc + PLAN_T - 1) / PLAN_T;
+  const int j0 = min(nloc, tid * chunk), j1 = min(nloc, j0 + chunk);
   int si = 0;
   for (int j = j0; j < j1; j++) si += (pl.cnt[j] + G - 1) / G;
   part[tid] = si;
@@ -967,78 +959,34 @@ __global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, c
   }
   int io = part[tid] - si;
   for (int j = j0; j < j1; j++) {
-    if (j == nloc) pl.n_items[9] = io;  // number of seed items
     const int c = pl.cnt[j];
     pl.ioff[j] = io;
     const int nit = (c + G - 1) / G;
-    const int l = lo + (j < nloc ? j : j - nloc);
-    const int64_t beg = nit ? list_off[l] : 0;
-    const int32_t sz = nit ? (int32_t)(list_off[l + 1] - beg) : 0;
-    const int64_t so = (nit && pl.soff) ? pl.soff[l] : 0;
+    const int64_t beg = nit ? list_off[lo + j] : 0;
+    const int32_t sz = nit ? (int32_t)(list_off[lo + j + 1] - beg) : 0;
     for (int t = 0; t < nit; t++) {
       int32_t* r = pl.recs + (int64_t)(io + t) * 16;
-      r[0] = l;
+      r[0] = lo + j;
       r[1] = min(G, c - t * G);
       r[2] = sz;
       r[3] = (int32_t)(uint32_t)(uint64_t)beg;
       r[4] = (int32_t)(uint32_t)((uint64_t)beg >> 32);
-      r[13] = (int32_t)(uint32_t)(uint64_t)so;
-      r[14] = (int32_t)(uint32_t)((uint64_t)so >> 32);
     }
     io += nit;
   }
   if (tid == PLAN_T - 1) pl.n_items[0] = part[PLAN_T - 1];
-  if (tid == 0 && nloc == 0) pl.n_items[9] = 0;
-  if (tid < 8) {  // per-XCD-group work counters of the scan launches
-    pl.n_items[1 + tid] = 0;
-    pl.n_items[17 + tid] = 0;
-  }
-}
-
-// This workgroup's items: its XCD group's share of the seed items [0, S), then
-// its share of the rest [S, N); contiguous shares keep the consecutive items of
-// one list (same T1 row, same codes) on one XCD's L2.  global_q: one queue.
-// pl.phase selects the items of this launch: 0 = all (seed items first), 1 = seed
-// items only, 2 = the rest only (a separate seed launch makes every bound tau_q
-// final before the bulk of the items start).
-struct ItemRange {
-  int s0, ns, r0, nr;
-  __device__ __forceinline__ int item(int v) const { return v < ns ? s0 + v : r0 + (v - ns); }
-  __device__ __forceinline__ int count() const { return ns + nr; }
-};
-__device__ __forceinline__ ItemRange item_range(const ListPlan& pl, bool global_q, int grp) {
-  const int N = pl.n_items[0], S = pl.n_items[9];
-  const int a0 = pl.phase == 2 ? S : 0, a1 = pl.phase == 1 ? S : N;  // items of this launch
-  const int S1 = min(max(S, a0), a1);                                 // seed items end here
-  ItemRange r;
-  if (global_q) {
-    r.s0 = a0;
-    r.ns = a1 - a0;
-    r.r0 = a1;
-    r.nr = 0;
-    return r;
-  }
-  const int ps = (S1 - a0 + 7) >> 3, pr = (a1 - S1 + 7) >> 3;
-  r.s0 = a0 + grp * ps;
-  r.ns = max(0, min(S1, r.s0 + ps) - r.s0);
-  r.r0 = S1 + grp * pr;
-  r.nr = max(0, min(a1, r.r0 + pr) - r.r0);
-  return r;
-}
-// per-launch work counters: n_items[1..8] (phase 0/1), n_items[17..24] (phase 2)
-__device__ __forceinline__ int* work_counter(const ListPlan& pl, int grp) {
-  return pl.n_items + (pl.phase == 2 ? 17 : 1) + grp;
+  if (tid < 8) pl.n_items[1 + tid] = 0;  // per-XCD-group work counters of phase B
 }
 
 // scatter each phase-B pair id into its work item record
 __global__ __launch_bounds__(256) void k_bucket_scatter(const int64_t* __restrict__ lists,
                                                         const float* __restrict__ dis0, int64_t nq, int nprobe, int lo,
-                                                        int hi, int G, ListPlan pl) {
+                                                        int G, ListPlan pl) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= nq * nprobe) return;
   const int s = pl.slot[i];
   if (s < 0) return;
-  const int item = pl.ioff[bucket_key(i, lists[i], nprobe, lo, hi, pl)] + s / G;
+  const int item = pl.ioff[(int)(lists[i] - lo)] + s / G;
   int32_t* r = pl.recs + (int64_t)item * 16;
   r[5 + s % G] = (int32_t)i;
   r[9 + s % G] = __float_as_int(dis0 ? dis0[i] : 0.f);
@@ -1110,10 +1058,13 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int k = a.k;
+  const int n_items = pl.n_items[0];
   // a.debug & 8: one global work counter (A/B against per-XCD-group counters)
   const bool global_q = (a.debug & 8) != 0;
+  const int per = global_q ? n_items : (n_items + 7) >> 3;
   const int grp = global_q ? 0 : (blockIdx.x & 7);
-  const ItemRange rng = item_range(pl, global_q, grp);
+  const int c0 = grp * per;
+  const int c1 = min(n_items, c0 + per);
   const uint64_t lanemask_lt = (1ull << lane) - 1;
 
   int it_no = 0;
@@ -1123,13 +1074,12 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
   };
   // dynamic work fetching inside the XCD group (items vary from 1 to ~3k codes)
   __shared__ int s_next;
-  int* ctr = work_counter(pl, grp);
-  if (tid == 0) s_next = atomicAdd(ctr, 1);
+  int* ctr = pl.n_items + 1 + grp;
+  if (tid == 0) s_next = c0 + atomicAdd(ctr, 1);
   __syncthreads();
-  for (int v = s_next; v < rng.count(); v = s_next, it_no++) {
+  for (int idx = s_next; idx < c1; idx = s_next, it_no++) {
     __syncthreads();  // everyone has read s_next
-    if (tid == 0) s_next = atomicAdd(ctr, 1);  // consumed after this item
-    const int idx = rng.item(v);
+    if (tid == 0) s_next = c0 + atomicAdd(ctr, 1);  // consumed after this item
     stamp(0, __builtin_amdgcn_s_memtime());
     // one self-contained record: no dependent metadata loads
     const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)idx * 16);
@@ -1327,347 +1277,6 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
     stamp(4, (uint64_t)n);
     stamp(5, (uint64_t)cnt);
     // each wave writes its own sorted partial list per query (no in-workgroup merge)
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      if (g >= cnt) continue;
-      const int64_t o = ((int64_t)pair[g] * 4 + wave) * k;
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        const int ix = r * 64 + lane;
-        if (ix < k) {
-          const bool empty = tk[g].id[r] == kSentinelId;
-          pl.partD[o + ix] = empty ? FLT_MAX : tk[g].d[r];
-          pl.partI[o + ix] = empty ? -1 : beg + tk[g].id[r];  // global code position
-        }
-      }
-    }
-    stamp(3, __builtin_amdgcn_s_memtime());
-    __syncthreads();  // s_next is visible
-  }
-}
-
-// ================================================= systolic list scan (M = 16, G = 4)
-// The gather loop of k_scan_lists has each lane look up sub-quantizer m of its
-// own code, so the 16 lanes of a ds_read_b128 lane group hit random bank slots
-// (~3.2-way conflicts: that kernel's bound).  Here lane (row, m) of a wave
-// ALWAYS reads sub-quantizer m = lane & 15 and the LUT image is [j][m][g]:
-// entry (j, m) at byte 256 j + 16 m, so every lane's bank slot is m, and each
-// lane group of a ds_read_b128 ({0-3,12-15,20-27}, ...) covers every m once:
-// conflict-free whatever the code bytes are.
-//
-// The codes flow through the lanes instead: each 16-lane DPP row is a systolic
-// pipeline.  At step s lane m adds term m of code (s - m) to the partial sum it
-// receives from lane m-1 (row_shr:1; lane 0 receives 0), so every distance is
-// summed in the oracle's order dis0 + tab[0][c0] + ... + tab[15][c15].  The
-// coarse term dis0 is folded into the m = 0 entries of the LUT
-// (fl(dis0 + tab0[j]) is exactly the first add of the sequential sum).  Lane 15
-// of each row holds one finished distance per step.
-//
-// Code image (ScanArgs::scodes, built by upload_lists): per list, chunks of
-// 256 B; in chunk b, lane m's 16 bytes hold byte m of codes 16 b + t - m,
-// t = 0..15 (zero outside the list).  Step t of super-step b reads byte t of the
-// lane's chunk: one coalesced 16-B load per lane per 16 steps and one v_perm per
-// step for the LDS address.  A list of n codes has ceil(n/16) + 1 chunks (the
-// last one drains the pipeline).  The 16 rows of a workgroup take contiguous
-// ranges of the list's 16-code blocks; a row starts with NaN partial sums, so
-// codes that began before its range never pass the admission test, and its
-// last (drain) super-step masks completions past its range.
-//
-// CBREG (d = 128, M = 16): T3 is formed in-kernel from the query and the
-// codebook slice each thread holds in registers for the whole launch (the same
-// 8-term tree as k_ip_table), instead of being read from the per-batch T3
-// buffer: 16 KiB of T3 per (query, probe) from the Infinity Cache becomes 512 B
-// of query plus VALU work.
-constexpr int SYS_M = 16;
-constexpr int SYS_G = 4;
-constexpr int SYS_PF = 4;  // code-chunk prefetch depth (super-steps)
-
-__device__ __forceinline__ float shr1z(float v) {
-  // row_shr:1 with bound_ctrl: lane 0 of each row reads 0
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
-}
-
-// <x[0..7], c[0..7]> in the Faiss AVX order of tree<K_IP> at dsub = 8:
-// ((p4 + p0) + (p5 + p1)) + ((p6 + p2) + (p7 + p3)), p_t = 0 + x_t c_t
-__device__ __forceinline__ float ip8(const float4 (&x)[2], const float4 (&c)[2]) {
-  const float p0 = 0.f + x[0].x * c[0].x, p1 = 0.f + x[0].y * c[0].y;
-  const float p2 = 0.f + x[0].z * c[0].z, p3 = 0.f + x[0].w * c[0].w;
-  const float p4 = 0.f + x[1].x * c[1].x, p5 = 0.f + x[1].y * c[1].y;
-  const float p6 = 0.f + x[1].z * c[1].z, p7 = 0.f + x[1].w * c[1].w;
-  const float h0 = (p4 + p0) + (p5 + p1);
-  const float h1 = (p6 + p2) + (p7 + p3);
-  return h0 + h1;
-}
-
-template <int R, bool CBREG>
-__global__ __launch_bounds__(256) void k_scan_sys(ScanArgs a, ListPlan pl) {
-  constexpr int M = SYS_M, G = SYS_G;
-  constexpr int LUT_BYTES = 256 * M * G * 4;  // 64 KiB
-  __shared__ __attribute__((aligned(16))) unsigned char lut[LUT_BYTES];
-  __shared__ float qd[4][QCAP];
-  __shared__ int32_t qi[4][QCAP];  // (code position in list << 2) | g
-  __shared__ float wkth[4][SYS_G];  // each wave's current k-th distance per query: shared admission bound
-  __shared__ int s_next;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int mm = lane & 15;  // this lane's sub-quantizer in the scan
-  const int row = lane >> 4;
-  const int mb = tid & 15;   // this thread's sub-quantizer in the LUT build
-  const int k = a.k;
-  const bool global_q = (a.debug & 8) != 0;
-  const int grp = global_q ? 0 : (blockIdx.x & 7);
-  const ItemRange rng = item_range(pl, global_q, grp);
-  const uint64_t lanemask_lt = (1ull << lane) - 1;
-
-  // LUT build: thread (mb, jq = tid/16 + 16 it) owns entries (mb, 4 jq + c): its
-  // T1/T3 reads are float4s, and its LDS stores of entries (j, mb) fill 16
-  // consecutive slots per lane group (conflict-free writes)
-  float4 cbv[CBREG ? 4 : 1][4][2];  // codebook rows of this thread's 16 entries (CBREG)
-  if constexpr (CBREG) {
-#pragma unroll
-    for (int it = 0; it < 4; it++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const int j = 4 * ((tid >> 4) + 16 * it) + c;
-        const float4* src = reinterpret_cast<const float4*>(a.cb + ((int64_t)mb * 256 + j) * 8);
-        cbv[it][c][0] = src[0];
-        cbv[it][c][1] = src[1];
-      }
-  }
-
-  int it_no = 0;
-  auto stamp = [&](int slot, uint64_t v) {
-    if (a.stamps && tid == 0 && it_no < kStampItems)
-      a.stamps[((int64_t)blockIdx.x * kStampItems + it_no) * kStampSlots + slot] = v;
-  };
-  int* ctr = work_counter(pl, grp);
-  if (tid == 0) s_next = atomicAdd(ctr, 1);
-  __syncthreads();
-  for (int v = s_next; v < rng.count(); v = s_next, it_no++) {
-    __syncthreads();  // everyone has read s_next
-    if (tid == 0) s_next = atomicAdd(ctr, 1);
-    const int idx = rng.item(v);
-    stamp(0, __builtin_amdgcn_s_memtime());
-    const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)idx * 16);
-    const int4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
-    const int64_t l = r0.x;
-    const int cnt = r0.y;
-    const int n = r0.z;
-    const int64_t beg = (int64_t)(((uint64_t)(uint32_t)r1.x << 32) | (uint32_t)r0.w);
-    const int64_t soff = (int64_t)(((uint64_t)(uint32_t)r3.z << 32) | (uint32_t)r3.y);
-    int pair[G];
-    int64_t qix[G];
-    float d0[G], bound[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      const int pr = g == 0 ? r1.y : g == 1 ? r1.z : g == 2 ? r1.w : r2.x;
-      const int db = g == 0 ? r2.y : g == 1 ? r2.z : g == 2 ? r2.w : r3.x;
-      pair[g] = g < cnt ? pr : 0;
-      qix[g] = pair[g] / a.nprobe;
-      d0[g] = __int_as_float(db);
-    }
-    float4 t1v[4];
-    float4 t3v[CBREG ? 1 : G][4];
-    float4 xv[CBREG ? G : 1][2];
-    {
-      const float* T1l = a.T1 + l * (M * 256) + mb * 256;
-#pragma unroll
-      for (int it = 0; it < 4; it++) t1v[it] = *reinterpret_cast<const float4*>(T1l + 4 * ((tid >> 4) + 16 * it));
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if constexpr (CBREG) {
-          const float4* xs = reinterpret_cast<const float4*>(a.xq + qix[g] * (M * 8) + mb * 8);
-          xv[g][0] = xs[0];
-          xv[g][1] = xs[1];
-        } else {
-          const float* T3q = a.T3 + qix[g] * (M * 256) + mb * 256;
-#pragma unroll
-          for (int it = 0; it < 4; it++)
-            t3v[g][it] = *reinterpret_cast<const float4*>(T3q + 4 * ((tid >> 4) + 16 * it));
-        }
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; g++) bound[g] = g < cnt ? __int_as_float(pl.tauq[qix[g]]) : -kInf;
-
-    // this lane's row: the 16 rows split the list's ceil(n/16) code blocks
-    const int nc = (n + 15) >> 4;
-    const int rid = wave * 4 + row;
-    const int rb0 = (nc * rid) >> 4, rb1 = (nc * (rid + 1)) >> 4;
-    int dmin = 1 << 30, dmax = 0;  // wave-uniform: block counts of the wave's 4 rows
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int x = wave * 4 + r;
-      const int dd = ((nc * (x + 1)) >> 4) - ((nc * x) >> 4);
-      dmin = min(dmin, dd);
-      dmax = max(dmax, dd);
-    }
-    const int cend = min(rb1 * 16, n);
-    const uint8_t* col = a.scodes + soff * 256 + mm * 16;
-    // code chunks are loaded SYS_PF super-steps ahead of their use (the first ones land during the LUT build)
-    uint4 cq[SYS_PF];
-#pragma unroll
-    for (int p = 0; p < SYS_PF; p++) cq[p] = *reinterpret_cast<const uint4*>(col + (int64_t)min(rb0 + p, nc) * 256);
-
-    __syncthreads();  // the previous item is done with the LDS
-    if (tid < 4 * G) wkth[tid / G][tid % G] = kInf;
-#pragma unroll
-    for (int it = 0; it < 4; it++) {
-      const int jq = (tid >> 4) + 16 * it;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        float4 o;
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          float t3;
-          if constexpr (CBREG)
-            t3 = ip8(xv[g], cbv[it][c]);
-          else
-            t3 = comp(t3v[g][it], c);
-          float val = comp(t1v[it], c) + (-2.0f * t3);
-          if (mb == 0) val = d0[g] + val;
-          setc(o, g, val);
-        }
-        *reinterpret_cast<float4*>(lut + (4 * jq + c) * 256 + mb * 16) = o;
-      }
-    }
-    __syncthreads();
-    stamp(1, __builtin_amdgcn_s_memtime());
-
-    WaveTopK<R> tk[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) tk[g].init(k);
-    int qn = 0;  // this wave's queue fill (wave-uniform)
-    // admission bounds live on the finishing lane (m = 15) of each row only
-    float bv[G];
-    auto set_bv = [&]() {
-#pragma unroll
-      for (int g = 0; g < G; g++) bv[g] = mm == 15 ? bound[g] : -kInf;
-    };
-    set_bv();
-
-    auto drain = [&]() {
-      for (int b0 = 0; b0 < qn; b0 += 64) {
-        const int e = b0 + lane;
-        const float cd = e < qn ? qd[wave][e] : kInf;
-        const int ci = e < qn ? qi[wave][e] : 0;
-        const int64_t pos = ci >> 2;
-        const int cg = ci & 3;
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          const bool p = e < qn && cg == g && lexless(cd, pos, tk[g].td, tk[g].ti);
-          const uint64_t mk = __ballot(p);
-          if (mk) {
-            if constexpr (R == 1) {
-              if (__popcll(mk) > 6)
-                bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : kSentinelId, lane);
-              else
-                tk[g].insert(mk, cd, pos, lane);
-            } else {
-              tk[g].insert(mk, cd, pos, lane);
-            }
-            bound[g] = fminf(bound[g], tk[g].td);
-          }
-        }
-      }
-      qn = 0;
-      // tighten the bounds with what the other waves (LDS) and workgroups (tau_q)
-      // have found: any k real candidates bound the final k-th distance
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if (g < cnt && tk[g].td < kInf && lane == 0) {
-          atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
-          wkth[wave][g] = tk[g].td;
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if (g < cnt) {
-          const float wb = fminf(fminf(wkth[0][g], wkth[1][g]), fminf(wkth[2][g], wkth[3][g]));
-          bound[g] = fminf(bound[g], fminf(wb, __int_as_float(pl.tauq[qix[g]])));
-        }
-      }
-      set_bv();
-    };
-
-    const uint32_t mbase = (uint32_t)mm << 4;
-    float P[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) P[g] = __builtin_nanf("");
-
-    // 16 steps of one super-step; CHECKED masks completions at or past cend.
-    // The LDS lookups of SB steps are issued before any of them is consumed:
-    // the candidate pushes store to LDS, so reads written after them in program
-    // order would each wait out the full LDS latency.
-    constexpr int SB = CBREG ? 8 : 16;
-    auto steps = [&](const uint4 cur, const int cb, auto checked_tag) {
-      constexpr bool CHECKED = decltype(checked_tag)::value;
-      const int lim = cend - cb;  // the completion of step t is code cb + t: valid iff t < lim
-#pragma unroll
-      for (int t0 = 0; t0 < 16; t0 += SB) {
-        float4 lvb[SB];
-#pragma unroll
-        for (int u = 0; u < SB; u++) {
-          const int t = t0 + u;
-          const uint32_t w = t < 4 ? cur.x : t < 8 ? cur.y : t < 12 ? cur.z : cur.w;
-          // (byte t of w) << 8 | m << 4 in one v_perm: {b0: mbase.b0, b1: w.b(t&3), b2, b3: 0}
-          const uint32_t sel = 0x0c0c0000u | ((uint32_t)(4 + (t & 3)) << 8);
-          const uint32_t addr = __builtin_amdgcn_perm(w, mbase, sel);
-          lvb[u] = *reinterpret_cast<const float4*>(lut + addr);
-        }
-#pragma unroll
-      for (int u = 0; u < SB; u++) {
-        const int t = t0 + u;
-        const float4 lv = lvb[u];
-        P[0] = shr1z(P[0]) + lv.x;
-        P[1] = shr1z(P[1]) + lv.y;
-        P[2] = shr1z(P[2]) + lv.z;
-        P[3] = shr1z(P[3]) + lv.w;
-        uint64_t mk[G];
-#pragma unroll
-        for (int g = 0; g < G; g++) mk[g] = __ballot(P[g] <= bv[g]);
-        uint64_t any = mk[0] | mk[1] | mk[2] | mk[3];
-        if constexpr (CHECKED) {
-          const uint64_t vm = __ballot(t < lim);
-          any &= vm;
-#pragma unroll
-          for (int g = 0; g < G; g++) mk[g] &= vm;
-        }
-        if (any) {
-          const int code = cb + t;
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            if ((mk[g] >> lane) & 1) {
-              const int sl = qn + __popcll(mk[g] & lanemask_lt);
-              qd[wave][sl] = P[g];
-              qi[wave][sl] = (code << 2) | g;
-            }
-            qn += __popcll(mk[g]);
-          }
-        }
-      }
-      }
-    };
-
-    for (int i = 0; i <= dmax; i++) {
-      const uint4 cur = cq[0];
-#pragma unroll
-      for (int p = 0; p + 1 < SYS_PF; p++) cq[p] = cq[p + 1];
-      cq[SYS_PF - 1] = *reinterpret_cast<const uint4*>(col + (int64_t)min(rb0 + i + SYS_PF, nc) * 256);
-      if (qn > 0) drain();  // a super-step pushes at most 16 steps x 4 rows x 4 queries = QCAP entries
-      const int cb = 16 * (rb0 + i) - 15;
-      if (i < dmin)
-        steps(cur, cb, std::false_type{});
-      else
-        steps(cur, cb, std::true_type{});
-    }
-    if (qn > 0) drain();
-
-    stamp(2, __builtin_amdgcn_s_memtime());
-    stamp(4, (uint64_t)n);
-    stamp(5, (uint64_t)cnt);
 #pragma unroll
     for (int g = 0; g < G; g++) {
       if (g >= cnt) continue;
@@ -1945,12 +1554,9 @@ int list_scan_group(int M, int k) {
   return G;
 }
 
-bool sys_scan_supported(int M, int k) { return M == SYS_M && rows_for(k) * SYS_G <= 16; }
-
 int list_scan_cap(int64_t nq, int nprobe, int nloc, int G) {
-  // sum over the 2 nloc keys of ceil(count / G) <= min(keys, pairs) + pairs / G
-  const int64_t p = nq * nprobe;
-  const int64_t v = std::min<int64_t>(2 * (int64_t)nloc, p) + (p + G - 1) / G + 8;
+  const int64_t p1 = nq * (nprobe > 1 ? nprobe - 1 : 0);
+  const int64_t v = std::min<int64_t>(nloc, p1) + (p1 + G - 1) / G + 8;
   return (int)(((v + 7) / 8) * 8);
 }
 
@@ -1958,23 +1564,15 @@ template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 16) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 16) ? 2 : 1;
   constexpr int J = M <= 8 ? 8 : M <= 16 ? SCAN_J16 : 2;  // codes per lane per batch (register budget)
+  ScanArgs seed = a;
+  seed.first_probe = pl.first_probe;
+  seed.partD = pl.partD;
+  seed.partI = pl.partI;
+  seed.tauq = pl.tauq;
+  seed.stamps = a.stamps ? a.stamps + (size_t)scan_lists_grid() * kStampItems * kStampSlots : nullptr;
+  if (pl.seed) hipLaunchKernelGGL((k_scan_topk<M, R, true>), dim3((unsigned)a.nq), dim3(256), 0, s, seed);
   if (ev) (void)hipEventRecord(ev[0], s);
-  // seed items in a launch of their own, then the rest (pl.seed == 0: one launch)
-  for (int ph = pl.seed ? 1 : 0; ph <= (pl.seed ? 2 : 0); ph++) {
-    ListPlan p = pl;
-    p.phase = ph;
-    bool done = false;
-    if constexpr (M == SYS_M && R * SYS_G <= 16) {
-      if (p.sys) {
-        if (p.cbreg)
-          hipLaunchKernelGGL((k_scan_sys<R, true>), dim3((unsigned)p.grid), dim3(256), 0, s, a, p);
-        else
-          hipLaunchKernelGGL((k_scan_sys<R, false>), dim3((unsigned)p.grid), dim3(256), 0, s, a, p);
-        done = true;
-      }
-    }
-    if (!done) hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)p.grid), dim3(256), 0, s, a, p);
-  }
+  hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   if (ev) (void)hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
@@ -2002,16 +1600,16 @@ static void launch_lists_M(const ScanArgs& a, const ListPlan& pl, hipStream_t s,
 
 void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev_lists) {
   if (a.nq <= 0) return;
-  const int G = pl.sys ? SYS_G : list_scan_group(a.M, a.k);
+  const int G = list_scan_group(a.M, a.k);
   const int64_t npairs = a.nq * a.nprobe;
   const int nloc = a.list_hi - a.list_lo;
-  hipLaunchKernelGGL(k_first_probe, dim3(nblocks(std::max<int64_t>(a.nq, 2 * (int64_t)nloc), 256)), dim3(256), 0,
-                     s, a.probe_list, a.nq, a.nprobe, a.list_off, a.list_lo, a.list_hi, pl);
+  hipLaunchKernelGGL(k_first_probe, dim3(nblocks(std::max<int64_t>(a.nq, (int64_t)nloc), 256)), dim3(256), 0, s,
+                     a.probe_list, a.nq, a.nprobe, a.list_off, a.list_lo, a.list_hi, pl);
   hipLaunchKernelGGL(k_bucket_count, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.nq, a.nprobe,
                      a.list_off, a.list_lo, a.list_hi, pl);
   hipLaunchKernelGGL(k_bucket_plan, dim3(1), dim3(PLAN_T), 0, s, a.list_lo, a.list_hi, G, a.list_off, pl);
   hipLaunchKernelGGL(k_bucket_scatter, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.probe_dis0,
-                     a.nq, a.nprobe, a.list_lo, a.list_hi, G, pl);
+                     a.nq, a.nprobe, a.list_lo, G, pl);
   switch (a.M) {
     case 8: launch_lists_M<8>(a, pl, s, ev_lists); break;
     case 16: launch_lists_M<16>(a, pl, s, ev_lists); break;

@@ -38,7 +38,7 @@ def main(d, key, out):
         if f is not None and w is not None:
             ent["hbm_bytes_per_launch"] = 2.0 * f * unit + w * unit
         res["kernels"][k] = ent
-    lists = [k for k in kernels if k.startswith("k_scan_sys")] or [k for k in kernels if k.startswith("k_scan_lists")]
+    lists = [k for k in kernels if k.startswith("k_scan_lists")]
     topk = [k for k in kernels if k.startswith("k_scan_topk") and "true" not in k]
     main_k = (lists or topk or [None])[0]
     res["kernel"] = main_k
