@@ -172,7 +172,12 @@ struct ivfpq_index {
     pl.seed = (debug & 64) ? 0 : 1;
     p_first.ensure(sizeof(int32_t) * nq);
     p_slot.ensure(sizeof(int32_t) * nq * np);
-    p_cnt.ensure(sizeof(int32_t) * std::max(nloc, 1));
+    if (!p_cnt.p || p_cnt.bytes < sizeof(int32_t) * std::max(nloc, 1)) {
+      // the counters are kept zero between batches by k_bucket_plan; zero them once here
+      p_cnt.ensure(sizeof(int32_t) * std::max(nloc, 1));
+      HIPCHECK(hipMemset(p_cnt.p, 0, p_cnt.bytes));
+      HIPCHECK(hipDeviceSynchronize());  // ordered before the (non-blocking) search stream uses them
+    }
     p_boff.ensure(sizeof(int32_t) * std::max(nloc, 1));
     p_it1.ensure(sizeof(int32_t) * 16 * pl.cap);
     p_nit.ensure(sizeof(int32_t) * 16);
@@ -193,7 +198,7 @@ struct ivfpq_index {
 
   // stage timing (HIP events recorded on the launch stream around each stage)
   enum Stage { ST_COARSE = 0, ST_TABLES = 1, ST_SCAN = 2, ST_LISTS = 3, ST_N = 4 };
-  bool timing = false;
+  int timing = 0;  // 0 off, 1 every stage, 2 the list-scan kernel only
   struct Mark {
     int stage;
     hipEvent_t a, b;  // adjacent: &a is passed as an event pair
@@ -212,10 +217,11 @@ struct ivfpq_index {
     return e;
   }
   // returns an index into marks (or -1 when timing is off)
-  int mark_begin(int stage, hipStream_t s) {
-    if (!timing) return -1;
+  // record = false: the caller records the pair itself (ST_LISTS, around one kernel)
+  int mark_begin(int stage, hipStream_t s, bool record = true) {
+    if (!timing || (timing == 2 && stage != ST_LISTS)) return -1;
     Mark m{stage, take_event(), take_event()};
-    HIPCHECK(hipEventRecord(m.a, s));
+    if (record) HIPCHECK(hipEventRecord(m.a, s));
     marks.push_back(m);
     return (int)marks.size() - 1;
   }
@@ -388,9 +394,12 @@ struct ivfpq_index {
   // coarse quantizer for c queries at x: nprobe nearest lists (fused kernel when
   // the per-query distance rows fit in LDS, else distance matrix + select)
   bool coarse_fused = true;  // IVFPQ_COARSE=split selects the two-kernel path (A/B)
-  void coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s) {
+  // plan (nullable): list-major plan whose bucket counting the fused kernel may take over
+  void coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
+                     ListPlan* plan = nullptr) {
     if (coarse_fused && nlist <= kCoarseFusedMax) {
-      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s);
+      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, plan,
+                          d_off.as<int64_t>(), list_lo, list_hi);
       return;
     }
     w_xn.ensure(sizeof(float) * c);
@@ -421,20 +430,33 @@ struct ivfpq_index {
       const float* xq = x + q0 * d;
       const int64_t* lists;
       const float* dis0;
+      ListPlan plan;
+      if (!query_major) plan = make_plan(c, np, k);
       if (preassigned) {
         lists = Iq + q0 * np;
         dis0 = Dq ? Dq + q0 * np : nullptr;
       } else {
         const int tm = mark_begin(ST_COARSE, s);
-        coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s);
+        coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s,
+                      (query_major || (debug & 128)) ? nullptr : &plan);
         mark_end(tm, s);
         lists = w_lists.as<int64_t>();
         dis0 = w_dis0.as<float>();
       }
-      const int tt = mark_begin(ST_TABLES, s);
-      launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
-      mark_end(tt, s);
+      // list-major with the seed pass: the seed launch builds T3 itself
+      const bool t3_in_seed = !query_major && !(debug & 64);
+      if (!t3_in_seed) {
+        const int tt = mark_begin(ST_TABLES, s);
+        launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
+        mark_end(tt, s);
+      }
       ScanArgs a;
+      if (t3_in_seed) {
+        a.xq = xq;
+        a.cb = d_cb.as<float>();
+        a.d = d;
+        a.T3out = w_T3.as<float>();
+      }
       a.T1 = d_T1.as<float>();
       a.T3 = w_T3.as<float>();
       a.codes = d_codes.as<uint8_t>();
@@ -462,8 +484,8 @@ struct ivfpq_index {
           a.stamps = w_stamps.as<uint64_t>();
         }
         // ST_LISTS: its two events are re-recorded around the list-scan kernel alone
-        const int tl = mark_begin(ST_LISTS, s);
-        launch_scan_lists(a, make_plan(c, np, k), s, tl >= 0 ? &marks[tl].a : nullptr);
+        const int tl = mark_begin(ST_LISTS, s, false);
+        launch_scan_lists(a, plan, s, tl >= 0 ? &marks[tl].a : nullptr);
         if (!stamp_out.empty()) {
           std::vector<uint64_t> hs(sb / 8);
           HIPCHECK(hipMemcpyAsync(hs.data(), w_stamps.p, sb, hipMemcpyDeviceToHost, s));
@@ -804,7 +826,8 @@ int ivfpq_set_timing(ivfpq_index* h, int on) {
   return guarded([&] {
     check_handle(h);
     std::lock_guard<std::mutex> lk(h->mu);
-    h->timing = on != 0;
+    require(on >= 0 && on <= 2, "timing mode must be 0, 1 or 2");
+    h->timing = on;
   });
 }
 

@@ -26,8 +26,12 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
 // launch_select_rows.
 constexpr int kCoarseFusedMax = 8192;
 void set_coarse_debug(int v);  // timing ablations of the fused coarse kernel (wrong results)
+struct ListPlan;
+// plan (nullable): also count the list-major buckets for `plan` (shard range [lo, hi)) in the epilogue;
+// sets plan->counted when it does (nprobe <= 64)
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s);
+                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, ListPlan* plan = nullptr,
+                         const int64_t* list_off = nullptr, int lo = 0, int hi = 0);
 
 // T3[q][m][j] = <x_q[m], C_mj>  (Faiss AVX order)
 void launch_ip_table(const float* x, int64_t n, int d, const float* codebook, int M, int ksub, float* out,
@@ -66,6 +70,17 @@ struct ScanArgs {
   int32_t* tauq = nullptr;  // seed mode also publishes each query's k-th distance here
   int debug = 0;            // timing ablations only (wrong results): 1 = no phase-B top-k, 2 = no LUT reads
   uint64_t* stamps = nullptr;  // diagnostic in-kernel s_memtime stamps (phase B), null in production
+  // List-major path: the seed launch builds T3 itself (no k_ip_table launch) from
+  // the queries and the codebook and stores it to T3out for the list scan.
+  const float* xq = nullptr;  // [nq][d]
+  const float* cb = nullptr;  // [M][ksub][dsub]
+  int d = 0;
+  float* T3out = nullptr;     // [nq][M][ksub]; null: T3 is read from T3
+  // Seed launch only: scatter pair ids into the list-scan work items (k_bucket_scatter's job)
+  const int32_t* scat_slot = nullptr;
+  const int32_t* scat_ioff = nullptr;
+  int32_t* scat_recs = nullptr;
+  int scat_G = 1;
 };
 constexpr int kStampItems = 32;  // items stamped per phase-B workgroup
 constexpr int kStampSlots = 6;   // per item: start, LUT ready, scan done, merge done, n, cnt
@@ -80,7 +95,7 @@ bool scan_supported_M(int M);
 struct ListPlan {
   int32_t* first_probe;  // [nq]
   int32_t* slot;         // [nq * nprobe]
-  int32_t* cnt;          // [nloc]
+  int32_t* cnt;          // [nloc]  zero between batches (k_bucket_plan re-zeroes after reading)
   int32_t* ioff;         // [nloc]  first work item of each list
   int32_t* recs;         // [cap][16] work item: list, count, size, offset(2), pairs(4), coarse dist(4)
   int32_t* n_items;      // [1]
@@ -90,6 +105,7 @@ struct ListPlan {
   int cap;               // upper bound on the number of work items
   int grid;              // persistent phase-B workgroups (multiple of 8)
   int seed = 1;          // run the threshold-seed pass (0: every probe in phase B)
+  int counted = 0;       // first_probe / tauq / slot / cnt already produced by the coarse epilogue
 };
 int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
 // phase-B item-count upper bound for a batch (host side, to size ListPlan)

@@ -342,6 +342,70 @@ __device__ __forceinline__ void wave_kway(float (&d)[KL], int64_t (&id)[KL], int
   }
 }
 
+// Threshold pre-filter for the same selection (lanes' 16 entries unsorted):
+// T = the k-th smallest of the 64 lane minima bounds the k-th smallest entry
+// (those k minima are k distinct entries <= T), so every entry of the top-k by
+// (dist, id) -- ties at T included -- has dist <= T.  When at most 64 entries
+// pass, they are compacted through `scratch` (>= 128 words of this wave's LDS,
+// no longer needed) and one 64-lane bitonic sort emits the k smallest in lanes
+// 0..k-1, exactly as wave_kway does.  Returns false (nothing written) when more
+// than 64 pass; the caller then runs lane_sort + wave_kway.
+__device__ __forceinline__ bool wave_select_threshold(const float (&d)[16], const int64_t (&id)[16], int k, int lane,
+                                                      float* scratch, float& out_d, int64_t& out_id) {
+  float m = d[0];
+#pragma unroll
+  for (int u = 1; u < 16; u++) m = fminf(m, d[u]);
+  // ascending bitonic sort of the lane minima (values only)
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      float o;
+      switch (j) {
+        case 1: o = xor_f<1>(m); break;
+        case 2: o = xor_f<2>(m); break;
+        case 4: o = xor_f<4>(m); break;
+        case 8: o = xor_f<8>(m); break;
+        case 16: o = xor_f<16>(m); break;
+        default: o = xor_f<32>(m); break;
+      }
+      const bool up = (lane & kk) == 0 || kk == 64;
+      const bool lower = (lane & j) == 0;
+      m = (lower == up) ? fminf(m, o) : fmaxf(m, o);
+    }
+  }
+  const float T = readlane_f(m, k - 1);
+  int c = 0;
+#pragma unroll
+  for (int u = 0; u < 16; u++) c += d[u] <= T ? 1 : 0;
+  // inclusive wave prefix sum of the per-lane counts
+  int incl = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  if (total > 64) return false;
+  int pos = incl - c;
+  int32_t* sid = reinterpret_cast<int32_t*>(scratch + 64);
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    if (d[u] <= T) {
+      scratch[pos] = d[u];
+      sid[pos] = (int32_t)id[u];  // list numbers (< 2^31)
+      pos++;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  float cd = lane < total ? scratch[lane] : kInf;
+  int64_t ci = lane < total ? (int64_t)sid[lane] : kSentinelId;
+  bitonic_sort64<2>(cd, ci, lane);
+  out_d = lane < k ? cd : kInf;
+  out_id = lane < k ? ci : kSentinelId;
+  return true;
+}
+
 // ------------------------------------------------------------------ norms
 __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int d,
                                                    float* __restrict__ out) {
@@ -421,13 +485,22 @@ __global__ __launch_bounds__(256) void k_l2_dist(const float* __restrict__ x, co
 // query w's nprobe nearest lists (same rule and arithmetic as k_l2_dist +
 // k_select_rows).
 constexpr int CQ = 4;
-__device__ int g_coarse_debug = 0;  // 1: skip the distance loop, 2: skip the selection (timing only)
+__device__ int g_coarse_debug = 0;
+
+// Optional list-major planning folded into the coarse epilogue (nprobe <= 64):
+// per query the first usable probe, tau_q reset and the per-list pair counts
+// of k_first_probe + k_bucket_count.
+struct CoarsePlan {
+  const int64_t* list_off = nullptr;  // null: no planning
+  int lo = 0, hi = 0;
+  ListPlan pl;
+};  // 1: skip the distance loop, 2: skip the selection (timing only)
 
 template <int R>
 __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
                                                       const float* __restrict__ centT, const float* __restrict__ cn,
                                                       int nlist, int nprobe, float* __restrict__ out_dis,
-                                                      int64_t* __restrict__ out_list) {
+                                                      int64_t* __restrict__ out_list, CoarsePlan cp) {
   extern __shared__ __attribute__((aligned(16))) float cs_mem[];
   float* xs = cs_mem;                       // [CQ][d]
   float* xn = xs + CQ * d;                  // [CQ]
@@ -498,7 +571,7 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
   if (q >= nq) return;
   WaveTopK<R> tk;
   tk.init(nprobe);
-  const float* drow = dist + wave * nlist;
+  float* drow = dist + wave * nlist;  // LDS row of this wave's query
   if (g_coarse_debug & 2) {
     if (lane < nprobe) {
       out_dis[q * nprobe + lane] = drow[lane];
@@ -520,10 +593,13 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
         cd[u] = cix < nlist ? drow[cix] : kInf;
         ci[u] = cix < nlist ? (int64_t)cix : kSentinelId;
       }
-      lane_sort<16>(cd, ci);
       float bd;
       int64_t bi;
-      wave_kway<16>(cd, ci, nprobe, lane, bd, bi);
+      // drow[0, 128) is free scratch once this block's entries are in registers
+      if (nlist < 128 || !wave_select_threshold(cd, ci, nprobe, lane, drow, bd, bi)) {
+        lane_sort<16>(cd, ci);
+        wave_kway<16>(cd, ci, nprobe, lane, bd, bi);
+      }
       if (base == 0) {
         rd = bd;
         ri = bi;
@@ -541,6 +617,18 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
       const bool empty = ri == kSentinelId;
       out_dis[q * nprobe + lane] = empty ? FLT_MAX : rd;
       out_list[q * nprobe + lane] = empty ? -1 : ri;
+    }
+    if (cp.list_off) {  // same rules as k_first_probe + k_bucket_count
+      const int64_t l = ri;  // kSentinelId when empty: outside [lo, hi)
+      const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
+      const uint64_t um = __ballot(use);
+      const int fp = (cp.pl.seed && um) ? (int)__builtin_ctzll(um) : nprobe;
+      if (lane == 0) {
+        cp.pl.first_probe[q] = fp;
+        cp.pl.tauq[q] = __float_as_int(kInf);
+      }
+      if (lane < nprobe)
+        cp.pl.slot[q * nprobe + lane] = (use && lane != fp) ? atomicAdd(&cp.pl.cnt[(int)(l - cp.lo)], 1) : -1;
     }
     return;
   }
@@ -739,6 +827,19 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
   const int wave = tid >> 6;
   const int64_t q = blockIdx.x;
   const int k = a.k;
+  if (a.scat_recs) {
+    // seed launch with the bucket scatter folded in (replaces k_bucket_scatter):
+    // this query's non-seed pairs go into their work item records
+    for (int p = tid; p < a.nprobe; p += 256) {
+      const int64_t i = q * a.nprobe + p;
+      const int sl = a.scat_slot[i];
+      if (sl < 0) continue;
+      const int G = a.scat_G;
+      int32_t* r = a.scat_recs + (int64_t)(a.scat_ioff[(int)(a.probe_list[i] - a.list_lo)] + sl / G) * 16;
+      r[5 + sl % G] = (int32_t)i;
+      r[9 + sl % G] = __float_as_int(a.probe_dis0 ? a.probe_dis0[i] : 0.f);
+    }
+  }
   // diagnostic stamps (seed mode): [q][4] = start, LUT ready, scan done, end
   auto qstamp = [&](int slot) {
     if (a.stamps && threadIdx.x == 0) a.stamps[q * 4 + slot] = __builtin_amdgcn_s_memtime();
@@ -747,7 +848,40 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
 
   // This thread's slice of the query's T3 (float4 index e*256 + tid).
   float4 t3[NV4];
-  {
+  if (a.T3out) {
+    // seed mode with the table build folded in (replaces k_ip_table): entries
+    // 4(e*256+tid)+c, same k_ip_table tree, stored for the list scan
+    float* xs = lut;  // the query, staged in the (not yet used) LUT space; d <= M * 256
+    for (int e = tid; e < a.d; e += 256) xs[e] = a.xq[q * a.d + e];
+    __syncthreads();
+    const int dsub = a.d / M;
+#pragma unroll
+    for (int e = 0; e < NV4; e++) {
+      const int e4 = 4 * (e * 256 + tid);
+      const float* xm = xs + (e4 >> 8) * dsub;  // the 4 entries share m (256 per m)
+      float v[4];
+      if (dsub == 8) {
+        const float4* src = reinterpret_cast<const float4*>(a.cb + (int64_t)e4 * 8);
+        float4 cw[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) cw[u] = src[u];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const float* w = reinterpret_cast<const float*>(&cw[2 * c]);
+          v[c] = tree<K_IP>([&](int t) { return xm[t]; }, [&](int t) { return w[t]; }, 8);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const float* w = a.cb + (int64_t)(e4 + c) * dsub;
+          v[c] = tree<K_IP>([&](int t) { return xm[t]; }, [&](int t) { return w[t]; }, dsub);
+        }
+      }
+      t3[e] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(a.T3out + q * LUTN)[e * 256 + tid] = t3[e];
+    }
+    // the LUT build below overwrites xs only after the loop's first barrier
+  } else {
     const float4* T3q = reinterpret_cast<const float4*>(a.T3 + q * LUTN);
 #pragma unroll
     for (int e = 0; e < NV4; e++) t3[e] = T3q[e * 256 + tid];
@@ -960,6 +1094,7 @@ __global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, c
   int io = part[tid] - si;
   for (int j = j0; j < j1; j++) {
     const int c = pl.cnt[j];
+    pl.cnt[j] = 0;  // invariant: counters are zero between batches (the coarse epilogue counts into them)
     pl.ioff[j] = io;
     const int nit = (c + G - 1) / G;
     const int64_t beg = nit ? list_off[lo + j] : 0;
@@ -1469,8 +1604,17 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
 void set_coarse_debug(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_coarse_debug), &v, sizeof(int)); }
 
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s) {
+                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, ListPlan* plan,
+                         const int64_t* list_off, int lo, int hi) {
   if (nq <= 0) return;
+  CoarsePlan cp;
+  if (plan && nprobe <= 64) {
+    cp.list_off = list_off;
+    cp.lo = lo;
+    cp.hi = hi;
+    cp.pl = *plan;
+    plan->counted = 1;
+  }
   const size_t smem = sizeof(float) * (CQ * d + CQ + (size_t)CQ * nlist);
   const dim3 grid(nblocks(nq, CQ));
   static bool attr_set = false;
@@ -1484,11 +1628,11 @@ void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, 
     attr_set = true;
   }
   switch (rows_for(nprobe)) {
-    case 1: hipLaunchKernelGGL(k_coarse_fused<1>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
-    case 2: hipLaunchKernelGGL(k_coarse_fused<2>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
-    case 4: hipLaunchKernelGGL(k_coarse_fused<4>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
-    case 8: hipLaunchKernelGGL(k_coarse_fused<8>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
-    default: hipLaunchKernelGGL(k_coarse_fused<16>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list); break;
+    case 1: hipLaunchKernelGGL(k_coarse_fused<1>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
+    case 2: hipLaunchKernelGGL(k_coarse_fused<2>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
+    case 4: hipLaunchKernelGGL(k_coarse_fused<4>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
+    case 8: hipLaunchKernelGGL(k_coarse_fused<8>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
+    default: hipLaunchKernelGGL(k_coarse_fused<16>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
   }
 }
 
@@ -1603,19 +1747,29 @@ void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hip
   const int G = list_scan_group(a.M, a.k);
   const int64_t npairs = a.nq * a.nprobe;
   const int nloc = a.list_hi - a.list_lo;
-  hipLaunchKernelGGL(k_first_probe, dim3(nblocks(std::max<int64_t>(a.nq, (int64_t)nloc), 256)), dim3(256), 0, s,
-                     a.probe_list, a.nq, a.nprobe, a.list_off, a.list_lo, a.list_hi, pl);
-  hipLaunchKernelGGL(k_bucket_count, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.nq, a.nprobe,
-                     a.list_off, a.list_lo, a.list_hi, pl);
+  if (!pl.counted) {  // else done by the coarse epilogue (launch_coarse_fused with a plan)
+    hipLaunchKernelGGL(k_first_probe, dim3(nblocks(std::max<int64_t>(a.nq, (int64_t)nloc), 256)), dim3(256), 0, s,
+                       a.probe_list, a.nq, a.nprobe, a.list_off, a.list_lo, a.list_hi, pl);
+    hipLaunchKernelGGL(k_bucket_count, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.nq, a.nprobe,
+                       a.list_off, a.list_lo, a.list_hi, pl);
+  }
   hipLaunchKernelGGL(k_bucket_plan, dim3(1), dim3(PLAN_T), 0, s, a.list_lo, a.list_hi, G, a.list_off, pl);
-  hipLaunchKernelGGL(k_bucket_scatter, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.probe_dis0,
-                     a.nq, a.nprobe, a.list_lo, G, pl);
+  ScanArgs b = a;
+  if (pl.seed) {  // the seed launch scatters the pairs into the item records
+    b.scat_slot = pl.slot;
+    b.scat_ioff = pl.ioff;
+    b.scat_recs = pl.recs;
+    b.scat_G = G;
+  } else {
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.probe_dis0,
+                       a.nq, a.nprobe, a.list_lo, G, pl);
+  }
   switch (a.M) {
-    case 8: launch_lists_M<8>(a, pl, s, ev_lists); break;
-    case 16: launch_lists_M<16>(a, pl, s, ev_lists); break;
-    case 32: launch_lists_M<32>(a, pl, s, ev_lists); break;
-    case 48: launch_lists_M<48>(a, pl, s, ev_lists); break;
-    case 64: launch_lists_M<64>(a, pl, s, ev_lists); break;
+    case 8: launch_lists_M<8>(b, pl, s, ev_lists); break;
+    case 16: launch_lists_M<16>(b, pl, s, ev_lists); break;
+    case 32: launch_lists_M<32>(b, pl, s, ev_lists); break;
+    case 48: launch_lists_M<48>(b, pl, s, ev_lists); break;
+    case 64: launch_lists_M<64>(b, pl, s, ev_lists); break;
     default: break;
   }
 }

@@ -367,8 +367,9 @@ class IndexIVFPQ:
     # ------------------------------------------------------------ stage timing
     STAGES = ("coarse", "tables", "scan", "lists")
 
-    def set_timing(self, on=True):
-        _lib.check(_lib.load().ivfpq_set_timing(self._h, 1 if on else 0))
+    def set_timing(self, on=True, lists_only=False):
+        """Record HIP events around every stage (or, lists_only, around the list-scan kernel alone)."""
+        _lib.check(_lib.load().ivfpq_set_timing(self._h, (2 if lists_only else 1) if on else 0))
 
     def get_timing(self):
         """{stage: (total_ms, launches)} since the last call (waits for the events)."""

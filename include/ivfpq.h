@@ -97,7 +97,9 @@ int ivfpq_merge_topk_device(int S, int64_t n, int k, const float* Din, const int
  * get_timing waits for the recorded events, returns per-stage sums in ms and launch counts
  * for stages {0: coarse probe, 1: inner-product table T3, 2: LUT + scan + top-k (all of it:
  * bucketing, seed pass, list scan, probe merge), 3: the list-scan kernel k_scan_lists alone
- * (list-major path; count 0 otherwise)}; both arrays hold 4 entries.  Resets. */
+ * (list-major path; count 0 otherwise)}; both arrays hold 4 entries.  Resets.
+ * on = 1: all stages; on = 2: only stage 3 (two events per batch: each recorded event
+ * costs a few microseconds of stream time, so throughput runs time the list scan alone). */
 int ivfpq_set_timing(ivfpq_index* h, int on);
 int ivfpq_get_timing(ivfpq_index* h, double* ms, int64_t* count);
 
