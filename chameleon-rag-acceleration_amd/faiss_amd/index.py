@@ -27,7 +27,7 @@ import re
 
 import numpy as np
 
-from . import _lib
+from . import _lib, faiss_io
 
 METRIC_INNER_PRODUCT = 0
 METRIC_L2 = 1
@@ -477,12 +477,39 @@ class ParameterSpace:
             self.set_index_parameter(index, name.strip(), float(value))
 
 
-def write_index(index, path):
-    _lib.check(_lib.load().ivfpq_save(index._h, str(path).encode()))
+def write_index(index, path, fmt="faiss"):
+    """Persist ``index``.  fmt "faiss": the Faiss 1.7.1 IndexIVFPQ binary layout
+    (``faiss.read_index`` loads it; faiss_io.py); "native": this library's CHIVFPQ1
+    image (also keeps untrained indexes)."""
+    if fmt == "native" or not index.is_trained:
+        _lib.check(_lib.load().ivfpq_save(index._h, str(path).encode()))
+        return
+    if fmt != "faiss":
+        raise RuntimeError(f"unknown index file format {fmt!r}")
+    inv = index.invlists
+    lists = [(inv.get_ids(l), inv.get_codes(l).reshape(-1, index.code_size)) for l in range(index.nlist)]
+    buf = faiss_io.serialize_ivfpq(index.d, index.nlist, index.nprobe, index.M, index.nbits, index.metric_type,
+                                   index.centroids(), index.codebook(), lists)
+    with open(path, "wb") as f:
+        f.write(buf)
 
 
 def read_index(path, device=None):
+    """Load a Faiss IndexIVFPQ file ("IwPQ") or a CHIVFPQ1 image onto ``device``."""
     device = _default_device() if device is None else device
+    if faiss_io.is_faiss_file(path):
+        with open(path, "rb") as f:
+            z = faiss_io.parse_ivfpq(f.read())
+        idx = IndexIVFPQ(None, z["d"], z["nlist"], z["M"], z["nbits"], z["metric"], device)
+        if z["is_trained"]:
+            idx.set_trained(z["centroids"], z["codebook"])
+            nonempty = [(l, ids, codes) for l, (ids, codes) in enumerate(z["lists"]) if len(ids)]
+            if nonempty:
+                idx.add_preencoded(np.concatenate([np.full(len(ids), l, np.int64) for l, ids, _ in nonempty]),
+                                   np.concatenate([codes for _, _, codes in nonempty]),
+                                   np.concatenate([ids for _, ids, _ in nonempty]))
+        idx.nprobe = max(1, min(int(z["nprobe"]), z["nlist"]))
+        return idx
     h = _lib.c_handle()
     L = _lib.load()
     _lib.check(L.ivfpq_load(str(path).encode(), device, ctypes.byref(h)))

@@ -259,13 +259,17 @@ def test_flat_search_exact():
         np.testing.assert_array_equal(D[q], dd[q][o].astype(np.float32))
 
 
-def test_save_load_roundtrip(tmp_path, golden_dir):
+@pytest.mark.parametrize("fmt", ["faiss", "native"])
+def test_save_load_roundtrip(tmp_path, golden_dir, fmt):
     z = load_case(golden_dir, "d96_m8_dsub12")
     ix = gpu_index(z)
-    p = tmp_path / "x.chivfpq"
-    faiss.write_index(ix, p)
+    p = tmp_path / f"x.{fmt}"
+    faiss.write_index(ix, p, fmt=fmt)
     iy = faiss.read_index(p, device=0)
     assert iy.ntotal == ix.ntotal and iy.nprobe == ix.nprobe
+    for l in range(ix.nlist):
+        np.testing.assert_array_equal(iy.invlists.get_ids(l), ix.invlists.get_ids(l))
+        np.testing.assert_array_equal(iy.invlists.get_codes(l), ix.invlists.get_codes(l))
     D, I = iy.search(z["xq"], int(z["k"]))
     assert_same(D, I, z["or_D"], z["or_I"])
 
