@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=10240, help="queries in the CPU-baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (repetitions)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--event-every", type=int, default=5,
+                   help="record the list-scan HIP events on every N-th timed step")
     p.add_argument("--no-recall", action="store_true")
     p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_scan_pmc.json"))
     return p.parse_args()
@@ -148,15 +150,15 @@ def main():
         dist.barrier()
     log(f"setup {time.time() - t_setup:.1f}s; timing {args.steps} steps")
 
-    # timed region: HIP events around the list-scan kernel only (each recorded
-    # event costs a few microseconds of stream time; the full stage split is
-    # measured in a separate pass below)
-    ix.set_timing(True, lists_only=True)
+    # timed region: HIP events around the list-scan kernel only, on every
+    # --event-every-th step (each recorded event costs ~6 us of stream time; the
+    # full stage split is measured in a separate pass below)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
+        ix.set_timing(s % args.event_every == 0, lists_only=True)
         step(s % args.nbatches)
     torch.cuda.synchronize()
     if world > 1:
@@ -186,7 +188,8 @@ def main():
     if lists_n > 0:  # list-major path: the dominant kernel is k_scan_lists
         kernel = f"k_scan_lists<{args.M},...> (phase-B list-major LUT + PQ scan + top-k)"
         avg_launch_ms = lists_ms / lists_n
-        bytes_per_launch = sum(bytes_lists[s % args.nbatches] for s in range(args.steps)) / args.steps
+        timed = [s for s in range(args.steps) if s % args.event_every == 0]  # the steps with events
+        bytes_per_launch = sum(bytes_lists[s % args.nbatches] for s in timed) / len(timed)
     else:  # IVFPQ_SCAN=query: one fused query-major kernel
         kernel = f"k_scan_topk<{args.M},...> (query-major fused LUT + PQ scan + top-k)"
         avg_launch_ms = scan_avg_ms
