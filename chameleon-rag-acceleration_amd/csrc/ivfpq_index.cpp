@@ -399,7 +399,8 @@ struct ivfpq_index {
                      ListPlan* plan = nullptr) {
     if (coarse_fused && nlist <= kCoarseFusedMax) {
       launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, plan,
-                          d_off.as<int64_t>(), list_lo, list_hi);
+                          d_off.as<int64_t>(), list_lo, list_hi, plan ? w_T3.as<float>() : nullptr,
+                          d_cb.as<float>(), M);
       return;
     }
     w_xn.ensure(sizeof(float) * c);
@@ -451,7 +452,7 @@ struct ivfpq_index {
         mark_end(tt, s);
       }
       ScanArgs a;
-      if (t3_in_seed) {
+      if (t3_in_seed && !plan.t3done) {
         a.xq = xq;
         a.cb = d_cb.as<float>();
         a.d = d;

@@ -31,7 +31,8 @@ struct ListPlan;
 // sets plan->counted when it does (nprobe <= 64)
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                          int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, ListPlan* plan = nullptr,
-                         const int64_t* list_off = nullptr, int lo = 0, int hi = 0);
+                         const int64_t* list_off = nullptr, int lo = 0, int hi = 0, float* T3out = nullptr,
+                         const float* codebook = nullptr, int M = 0);  // T3out: also build T3 (sets plan->t3done)
 
 // T3[q][m][j] = <x_q[m], C_mj>  (Faiss AVX order)
 void launch_ip_table(const float* x, int64_t n, int d, const float* codebook, int M, int ksub, float* out,
@@ -106,6 +107,7 @@ struct ListPlan {
   int grid;              // persistent phase-B workgroups (multiple of 8)
   int seed = 1;          // run the threshold-seed pass (0: every probe in phase B)
   int counted = 0;       // first_probe / tauq / slot / cnt already produced by the coarse epilogue
+  int t3done = 0;        // T3 already built by the coarse kernel
 };
 int list_scan_group(int M, int k);  // queries per work item (G) used for (M, k)
 // phase-B item-count upper bound for a batch (host side, to size ListPlan)

@@ -494,6 +494,10 @@ struct CoarsePlan {
   const int64_t* list_off = nullptr;  // null: no planning
   int lo = 0, hi = 0;
   ListPlan pl;
+  // also T3 for the workgroup's queries (k_ip_table's tree; the codebook is read once per 4 queries)
+  float* T3out = nullptr;
+  const float* cb = nullptr;
+  int M = 0;
 };  // 1: skip the distance loop, 2: skip the selection (timing only)
 
 template <int R>
@@ -517,6 +521,46 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
   if (tid < CQ) {
     const float* xr = xs + tid * d;
     xn[tid] = tree<K_NORM>([&](int t) { return xr[t]; }, [&](int t) { return xr[t]; }, d);
+  }
+  if (cp.T3out) {
+    const int dsub = d / cp.M;
+    const int total = cp.M * 256;
+    if (dsub == 8) {
+      // TB entries per round trip: all their codebook loads are issued before any tree
+      constexpr int TB = 4;
+      for (int e0 = tid; e0 < total; e0 += 256 * TB) {
+        float4 cw[TB][2];
+#pragma unroll
+        for (int b = 0; b < TB; b++) {
+          const float4* src = reinterpret_cast<const float4*>(cp.cb + (int64_t)min(e0 + b * 256, total - 1) * 8);
+          cw[b][0] = src[0];
+          cw[b][1] = src[1];
+        }
+#pragma unroll
+        for (int b = 0; b < TB; b++) {
+          const int e = e0 + b * 256;
+          if (e >= total) break;
+          const float* w = reinterpret_cast<const float*>(cw[b]);
+          const float* xm = xs + (e >> 8) * 8;
+#pragma unroll
+          for (int qq = 0; qq < CQ; qq++) {
+            if (q0 + qq >= nq) break;
+            const float* xq = xm + qq * d;
+            cp.T3out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
+          }
+        }
+      }
+    } else {
+      for (int e = tid; e < total; e += 256) {
+        const float* xm = xs + (e >> 8) * dsub;
+        const float* cwp = cp.cb + (int64_t)e * dsub;
+        for (int qq = 0; qq < CQ; qq++) {
+          if (q0 + qq >= nq) break;
+          const float* xq = xm + qq * d;
+          cp.T3out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
+        }
+      }
+    }
   }
   for (int cb0 = 0; cb0 < nlist; cb0 += 1024) {
     const int c4 = cb0 + 4 * tid;  // first of this thread's 4 centroids
@@ -1605,7 +1649,7 @@ void set_coarse_debug(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_coarse_debug
 
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                          int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, ListPlan* plan,
-                         const int64_t* list_off, int lo, int hi) {
+                         const int64_t* list_off, int lo, int hi, float* T3out, const float* cb, int M) {
   if (nq <= 0) return;
   CoarsePlan cp;
   if (plan && nprobe <= 64) {
@@ -1614,6 +1658,12 @@ void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, 
     cp.hi = hi;
     cp.pl = *plan;
     plan->counted = 1;
+  }
+  if (T3out && M > 0 && d % M == 0) {
+    cp.T3out = T3out;
+    cp.cb = cb;
+    cp.M = M;
+    if (plan) plan->t3done = 1;
   }
   const size_t smem = sizeof(float) * (CQ * d + CQ + (size_t)CQ * nlist);
   const dim3 grid(nblocks(nq, CQ));
