@@ -1508,8 +1508,10 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     }
 #pragma unroll
     for (int u = 0; u < 16; u++) {
+      // slots of unscanned probes (empty or foreign lists, lanes past nprobe) were never
+      // written this batch: their positions are stale memory and must not be dereferenced
       const bool ok = scanned && u < k && pos[u] >= 0;
-      const int64_t lab = a.ids[pos[u] >= 0 ? pos[u] : 0];
+      const int64_t lab = a.ids[ok ? pos[u] : 0];
       id[u] = ok ? lab : kSentinelId;
       d[u] = ok ? d[u] : kInf;
     }

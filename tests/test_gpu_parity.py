@@ -205,6 +205,28 @@ def test_train_and_encode_match_oracle():
     assert ix.quantizer.ntotal == 16
 
 
+def test_search_after_gpu_training_with_stale_workspaces():
+    """The smoke() shape: an index trained on the GPU (whose freed k-means buffers
+    leave non-zero memory behind) and searched at once, with probes landing on
+    lists that receive no codes.  Partial-result slots of unscanned probes are
+    never written, so the merge must not dereference them."""
+    xt = datasets.synthetic_sift_like(4000, 64, seed=4321, n_centres=100)
+    xb = datasets.synthetic_sift_like(20000, 64, seed=1234, n_centres=100)
+    xq = datasets.synthetic_sift_like(64, 64, seed=123, n_centres=100)
+    ix = faiss.index_factory(64, "IVF64,PQ16", device=0)
+    ix.niter_coarse = ix.niter_pq = 5
+    ix.train(xt)
+    ix.add(xb)
+    ix.nprobe = 8
+    D, I = ix.search(xq, 10)
+    ox = O.OracleIVFPQ(64, 64, 16)
+    ox.set_trained(ix.centroids(), ix.codebook())
+    ox.add(xb)
+    ox.nprobe = 8
+    Dr, Ir = ox.search(xq, 10)
+    assert_same(D, I, Dr, Ir)
+
+
 def test_device_entry_points_match_host(golden_dir):
     import torch
 
