@@ -1127,15 +1127,20 @@ __global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, c
   const int j0 = min(nloc, tid * chunk), j1 = min(nloc, j0 + chunk);
   int si = 0;
   for (int j = j0; j < j1; j++) si += (pl.cnt[j] + G - 1) / G;
-  part[tid] = si;
-  __syncthreads();
-  for (int off = 1; off < PLAN_T; off <<= 1) {
-    const int a = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += a;
-    __syncthreads();
+  // exclusive prefix sum over the workgroup: wave scans (shuffles), then the
+  // 16 wave totals through LDS (two barriers instead of twenty)
+  const int lane = tid & 63, wave = tid >> 6;
+  int incl = si;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
   }
-  int io = part[tid] - si;
+  if (lane == 63) part[wave] = incl;
+  __syncthreads();
+  int before = 0;
+  for (int w = 0; w < wave; w++) before += part[w];
+  int io = before + incl - si;
   for (int j = j0; j < j1; j++) {
     const int c = pl.cnt[j];
     pl.cnt[j] = 0;  // invariant: counters are zero between batches (the coarse epilogue counts into them)
@@ -1153,7 +1158,7 @@ __global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, c
     }
     io += nit;
   }
-  if (tid == PLAN_T - 1) pl.n_items[0] = part[PLAN_T - 1];
+  if (tid == PLAN_T - 1) pl.n_items[0] = before + incl;
   if (tid < 8) pl.n_items[1 + tid] = 0;  // per-XCD-group work counters of phase B
 }
 
