@@ -1,0 +1,183 @@
+"""GPU parity at the BASELINE.json config shapes (C1-C4) and for the list-range
+shard path, through the C-ABI, bit-exact against the CPU oracle.
+
+* C1 / C2: the SIFT1M-shaped index (nb = 1e6, IVF1024,PQ16) at nprobe 8 and 16.
+* C3-shaped: d = 768, M = 64 (64-B codes), nprobe = 32, k in {10, 1000}, at a
+  reduced base size (the kernels' M = 64 instantiations).
+* C4-shaped: d = 96, M = 48 (dsub 2), nlist = 65536 (the large-nlist coarse
+  path), nprobe = 32, at a reduced base size.
+* Shards: N in {2, 4} list-range handles on one GPU (set_list_range, as each
+  rank of bench.py's shard mode holds), partials merged on the device with
+  merge_topk_device; must equal the unsharded result (reference counterpart:
+  IndexShards, Chameleon/Faiss_experiments/bench_gpu_1bn.py:605-616, and the
+  host argsort merge of bench_multi_cpu_performance_OSDI.py:203-218).
+"""
+import numpy as np
+import pytest
+
+import faiss_amd as faiss
+from faiss_amd import datasets
+from faiss_amd.sharding import balanced_list_ranges
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def assert_same(D, I, Dr, Ir):
+    np.testing.assert_array_equal(I, Ir)
+    np.testing.assert_allclose(D, Dr, rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(D, Dr)
+
+
+def oracle_like(ix):
+    """Oracle index holding exactly the GPU index's trained quantizers and lists."""
+    ox = O.OracleIVFPQ(ix.d, ix.nlist, ix.M)
+    ox.set_trained(ix.centroids(), ix.codebook())
+    for l in range(ix.nlist):
+        ox.list_ids[l] = ix.invlists.get_ids(l)
+        ox.list_codes[l] = ix.invlists.get_codes(l).reshape(-1, ix.M)
+    ox.ntotal = ix.ntotal
+    ox.metric = ix.metric_type
+    return ox
+
+
+def build(d, nlist, M, nb, nt, nq, niter, metric=faiss.METRIC_L2, n_centres=10000):
+    xt = datasets.synthetic_sift_like(nt, d, seed=4321, n_centres=n_centres)
+    xb = datasets.synthetic_sift_like(nb, d, seed=1234, n_centres=n_centres)
+    xq = datasets.synthetic_sift_like(nq, d, seed=123, n_centres=n_centres)
+    ix = faiss.index_factory(d, f"IVF{nlist},PQ{M}", metric)
+    ix.niter_coarse = ix.niter_pq = niter
+    ix.train(xt)
+    ix.add(xb)
+    return ix, xq
+
+
+@pytest.fixture(scope="module")
+def sift1m():
+    ix, xq = build(128, 1024, 16, 1_000_000, 100_000, 1024, 8)
+    return ix, oracle_like(ix), xq
+
+
+@pytest.mark.parametrize("nprobe", [8, 16])
+def test_c1_c2_sift1m_shape(sift1m, nprobe):
+    """C1 (nprobe=8) and C2 (nprobe=16) on the 1e6-vector IVF1024,PQ16 index."""
+    ix, ox, xq = sift1m
+    ix.nprobe = ox.nprobe = nprobe
+    D, I = ix.search(xq, 10)
+    Dr, Ir = ox.search(xq, 10)
+    assert_same(D, I, Dr, Ir)
+
+
+def test_c2_k100(sift1m):
+    """k = 100, the reference's profiling K (MICRO_GPU_profiling)."""
+    ix, ox, xq = sift1m
+    ix.nprobe = ox.nprobe = 16
+    D, I = ix.search(xq[:512], 100)
+    Dr, Ir = ox.search(xq[:512], 100)
+    assert_same(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("nshards", [2, 4])
+def test_list_range_shards_c2(sift1m, nshards):
+    """N list-range handles on one GPU, each searching the whole batch on the
+    device; the stacked partials merged by merge_topk_device equal the
+    unsharded oracle result bit for bit."""
+    import torch
+
+    ix, ox, xq = sift1m
+    ox.nprobe = 16
+    sizes = ix.invlists.list_sizes()
+    ranges = balanced_list_ranges(sizes, nshards, ix.M)
+    xd = torch.from_numpy(xq).cuda()
+    Ds, Is = [], []
+    for lo, hi in ranges:
+        sh = faiss.IndexIVFPQ(None, ix.d, ix.nlist, ix.M, 8, device=0)
+        sh.set_trained(ix.centroids(), ix.codebook())
+        sh.set_list_range(lo, hi)
+        lists = [l for l in range(lo, hi) if sizes[l]]
+        sh.add_preencoded(np.concatenate([np.full(sizes[l], l, np.int64) for l in lists]),
+                          np.concatenate([ix.invlists.get_codes(l).reshape(-1, ix.M) for l in lists]),
+                          np.concatenate([ix.invlists.get_ids(l) for l in lists]))
+        sh.nprobe = 16
+        D, I = sh.search_device(xd, 10)
+        Ds.append(D)
+        Is.append(I)
+    D, I = faiss.merge_topk_device(torch.stack(Ds), torch.stack(Is))
+    torch.cuda.synchronize()
+    Dr, Ir = ox.search(xq, 10)
+    assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+
+
+@pytest.mark.parametrize("nshards", [2, 4])
+def test_list_range_shards_golden(golden_dir, nshards):
+    """Golden fixture, list ranges that include empty ranges (owning only empty
+    lists) and queries none of whose probes land in a range: those shards
+    return all-padding partials, and the slots of their unscanned probes are
+    never written (the merge must not read them)."""
+    import os
+
+    import torch
+
+    z = dict(np.load(os.path.join(golden_dir, "ivfpq_d128_m16.npz")))
+    d, M, nlist, nprobe, k = (int(z[n]) for n in ("d", "M", "nlist", "nprobe", "k"))
+    sizes = np.diff(z["list_off"])
+    list_no = np.repeat(np.arange(nlist, dtype=np.int64), sizes)
+    # an uneven cut: shard 0 owns only list 0, emptied below; the rest split the remainder
+    cuts = [0, 1] + [1 + (nlist - 1) * r // (nshards - 1) for r in range(1, nshards - 1)] + [nlist]
+    ranges = list(zip(cuts[:-1], cuts[1:]))
+    keep_all = list_no != 0  # list 0 receives no vectors
+    xd = torch.from_numpy(z["xq"]).cuda()
+    Ds, Is = [], []
+    for lo, hi in ranges:
+        sh = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+        sh.set_trained(z["centroids"], z["codebook"])
+        sh.set_list_range(lo, hi)
+        sel = keep_all & (list_no >= lo) & (list_no < hi)
+        if sel.any():
+            sh.add_preencoded(list_no[sel], z["codes"][sel], z["ids"][sel])
+        sh.nprobe = nprobe
+        D, I = sh.search_device(xd, k)
+        Ds.append(D)
+        Is.append(I)
+    torch.cuda.synchronize()
+    assert (Is[0].cpu().numpy() == -1).all()  # the empty shard
+    D, I = faiss.merge_topk_device(torch.stack(Ds), torch.stack(Is))
+    ox = O.OracleIVFPQ(d, nlist, M)
+    ox.set_trained(z["centroids"], z["codebook"])
+    ox.add_preencoded(list_no[keep_all], z["codes"][keep_all], z["ids"][keep_all])
+    ox.nprobe = nprobe
+    Dr, Ir = ox.search(z["xq"], k)
+    assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+
+
+@pytest.fixture(scope="module")
+def c3_shape():
+    # BEIR-NQ-shaped: 768-d, 64-B codes; nb reduced to 60k (C3 is 2.68M)
+    ix, xq = build(768, 256, 64, 60_000, 20_000, 64, 4, n_centres=2000)
+    return ix, oracle_like(ix), xq
+
+
+@pytest.mark.parametrize("k", [10, 1000])
+def test_c3_shape_m64_nprobe32(c3_shape, k):
+    ix, ox, xq = c3_shape
+    ix.nprobe = ox.nprobe = 32
+    D, I = ix.search(xq, k)
+    Dr, Ir = ox.search(xq, k)
+    assert_same(D, I, Dr, Ir)
+
+
+@pytest.fixture(scope="module")
+def c4_shape():
+    # Deep1B-shaped: d = 96, M = 48 (dsub 2), nlist = 65536; nb reduced to 400k (C4 is 1e9)
+    ix, xq = build(96, 65536, 48, 400_000, 70_000, 96, 2, n_centres=50000)
+    return ix, oracle_like(ix), xq
+
+
+@pytest.mark.parametrize("k", [10, 100])
+def test_c4_shape_m48_nlist65536(c4_shape, k):
+    ix, ox, xq = c4_shape
+    ix.nprobe = ox.nprobe = 32
+    D, I = ix.search(xq, k)
+    Dr, Ir = ox.search(xq, k)
+    assert_same(D, I, Dr, Ir)
