@@ -121,17 +121,14 @@ def main():
     Ibuf = torch.empty((Bg, k), dtype=torch.int64, device=dev)
 
     # algorithmic bytes: code_size x codes of every probed list in this
-    # rank's range, per batch; and the part the list-scan kernel covers (every probe
-    # but each query's first usable one, which the seed pass scans)
-    bytes_alg, bytes_lists = [], []
+    # rank's range, per batch; the list-scan kernel covers all of them
+    bytes_alg = []
     for b in range(args.nbatches):
         _, Iq = ix.coarse_device(xq_dev[b])
         Iq = Iq.cpu().numpy()
         sz = np.where(Iq >= 0, list_sizes[np.maximum(Iq, 0)], 0)  # lists outside [lo, hi) have size 0 here
-        first = np.argmax(sz > 0, axis=1)
-        seed = np.where(sz.max(axis=1) > 0, sz[np.arange(sz.shape[0]), first], 0)
         bytes_alg.append(int(sz.sum()) * args.M)
-        bytes_lists.append(int(sz.sum() - seed.sum()) * args.M)
+    bytes_lists = bytes_alg
 
     merged = {}
 
@@ -186,7 +183,7 @@ def main():
     lists_ms, lists_n = stages["lists"]
     bytes_per_step = sum(bytes_alg[s % args.nbatches] for s in range(args.steps)) / args.steps
     if lists_n > 0:  # list-major path: the dominant kernel is k_scan_lists
-        kernel = f"k_scan_lists<{args.M},...> (phase-B list-major LUT + PQ scan + top-k)"
+        kernel = f"k_scan_lists<{args.M},...> (list-major LUT + PQ scan + top-k, every probe)"
         avg_launch_ms = lists_ms / lists_n
         timed = [s for s in range(args.steps) if s % args.event_every == 0]  # the steps with events
         bytes_per_launch = sum(bytes_lists[s % args.nbatches] for s in timed) / len(timed)

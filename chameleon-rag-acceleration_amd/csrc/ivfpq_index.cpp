@@ -155,41 +155,51 @@ struct ivfpq_index {
   hipStream_t stream = nullptr;
   // scratch
   DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
-  // list-major scan plan workspaces
-  DevBuf p_first, p_slot, p_cnt, p_boff, p_it1, p_nit, p_D, p_I, p_tau;
-  bool query_major = false;
-  int debug = 0;  // IVFPQ_DEBUG: kernel timing ablations (wrong results)
-  std::string stamp_out;  // IVFPQ_STAMPS=<path>: dump phase-B in-kernel stamps (diagnostic)
-  DevBuf w_stamps;  // IVFPQ_SCAN=query selects the query-major kernel (A/B only)
+  // list-major plan workspaces (ivfpq_kernels.h ListPlan)
+  DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_tau;
+  // Stream ordering of the per-handle workspaces: every device search records
+  // `done` on its stream; the next search (on any stream) waits for it, and
+  // anything that frees or rewrites device buffers synchronizes on it first.
+  hipEvent_t done = nullptr;
+  hipStream_t done_stream = nullptr;
+  bool done_pending = false;
   std::mutex mu;
 
-  ListPlan make_plan(int64_t nq, int np, int k) {
-    const int nloc = list_hi - list_lo;
+  void order_after_last(hipStream_t s) {
+    if (done_pending && done_stream != s) HIPCHECK(hipStreamWaitEvent(s, done, 0));
+  }
+  void mark_done(hipStream_t s) {
+    HIPCHECK(hipEventRecord(done, s));
+    done_stream = s;
+    done_pending = true;
+  }
+  void quiesce() {
+    if (done_pending) HIPCHECK(hipEventSynchronize(done));
+    done_pending = false;
+  }
+
+  ListPlan make_plan(int64_t nq, int np, int k, hipStream_t s) {
+    const int nloc = std::max(list_hi - list_lo, 1);
     const int G = list_scan_group(M, k);
     ListPlan pl;
-    pl.cap = list_scan_cap(nq, np, nloc, G);
+    pl.cap = (int)nq;
+    pl.max_items = list_scan_max_items(nq * np, nloc, G);
     pl.grid = scan_lists_grid();
-    pl.seed = (debug & 64) ? 0 : 1;
-    p_first.ensure(sizeof(int32_t) * nq);
-    p_slot.ensure(sizeof(int32_t) * nq * np);
-    if (!p_cnt.p || p_cnt.bytes < sizeof(int32_t) * std::max(nloc, 1)) {
-      // the counters are kept zero between batches by k_bucket_plan; zero them once here
-      p_cnt.ensure(sizeof(int32_t) * std::max(nloc, 1));
-      HIPCHECK(hipMemset(p_cnt.p, 0, p_cnt.bytes));
-      HIPCHECK(hipDeviceSynchronize());  // ordered before the (non-blocking) search stream uses them
+    if (!p_cnt.p || p_cnt.bytes < sizeof(int32_t) * 2 * nloc) {
+      // kept zero between batches by k_scan_lists; zeroed once here
+      p_cnt.ensure(sizeof(int32_t) * 2 * nloc);
+      HIPCHECK(hipMemsetAsync(p_cnt.p, 0, p_cnt.bytes, s));
     }
-    p_boff.ensure(sizeof(int32_t) * std::max(nloc, 1));
-    p_it1.ensure(sizeof(int32_t) * 16 * pl.cap);
-    p_nit.ensure(sizeof(int32_t) * 16);
+    p_bucket.ensure(sizeof(int2) * 2 * (size_t)nloc * nq);
+    p_recs.ensure(sizeof(int32_t) * 16 * (size_t)pl.max_items);
+    p_hdr.ensure(sizeof(int32_t) * 16);
     p_D.ensure(sizeof(float) * nq * np * 4 * k);
     p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
     p_tau.ensure(sizeof(int32_t) * nq);
-    pl.first_probe = p_first.as<int32_t>();
-    pl.slot = p_slot.as<int32_t>();
     pl.cnt = p_cnt.as<int32_t>();
-    pl.ioff = p_boff.as<int32_t>();
-    pl.recs = p_it1.as<int32_t>();
-    pl.n_items = p_nit.as<int32_t>();
+    pl.bucket = p_bucket.as<int2>();
+    pl.recs = p_recs.as<int32_t>();
+    pl.hdr = p_hdr.as<int32_t>();
     pl.partD = p_D.as<float>();
     pl.partI = p_I.as<int64_t>();
     pl.tauq = p_tau.as<int32_t>();
@@ -251,18 +261,21 @@ struct ivfpq_index {
       (void)hipEventDestroy(m.b);
     }
     for (auto e : ev_pool) (void)hipEventDestroy(e);
+    if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
   void init_stream() {
     if (!stream) HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    if (!done) HIPCHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
   }
 
   // ---------------------------------------------------------------- helpers
   // Row-wise top-1 of x [n][dd] against c (already on device with norms):
   // writes assignments (host) for all rows. Uses w_x / w_xn / w_dist / w_D / w_I.
+  // ip: assign to the largest inner product (the IndexFlatIP quantizer of an IP index)
   void assign_top1(const float* x_host, int64_t n, int dd, const float* dc, const float* dcn, int nc,
-                   int64_t* assign_host, const float* x_dev = nullptr) {
+                   int64_t* assign_host, const float* x_dev = nullptr, bool ip_assign = false) {
     const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nc * 4)));
     w_xn.ensure(sizeof(float) * rows);
     w_dist.ensure(sizeof(float) * rows * nc);
@@ -278,8 +291,8 @@ struct ivfpq_index {
         HIPCHECK(hipMemcpyAsync(w_x.p, x_host + r0 * dd, sizeof(float) * c * dd, hipMemcpyHostToDevice, stream));
         xd = w_x.as<float>();
       }
-      launch_row_norms(xd, c, dd, w_xn.as<float>(), stream);
-      launch_l2_dist(xd, w_xn.as<float>(), c, dc, dcn, nc, dd, w_dist.as<float>(), stream);
+      if (!ip_assign) launch_row_norms(xd, c, dd, w_xn.as<float>(), stream);
+      launch_l2_dist(xd, w_xn.as<float>(), c, dc, dcn, nc, dd, w_dist.as<float>(), stream, ip_assign);
       launch_select_rows(w_dist.as<float>(), c, nc, 1, w_D.as<float>(), w_I.as<int64_t>(), stream);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipMemcpyAsync(assign_host + r0, w_I.p, sizeof(int64_t) * c, hipMemcpyDeviceToHost, stream));
@@ -287,7 +300,8 @@ struct ivfpq_index {
     }
   }
 
-  void kmeans(const float* x, int64_t n, int dd, int k, int niter, uint64_t seed, float* cent) {
+  void kmeans(const float* x, int64_t n, int dd, int k, int niter, uint64_t seed, float* cent,
+              bool ip_assign = false) {
     require(n >= k, "k-means: need at least as many training points as centroids (" + std::to_string(n) + " < " +
                         std::to_string(k) + ")");
     const auto init = rand_perm_prefix(n, k, seed);
@@ -306,12 +320,13 @@ struct ivfpq_index {
       HIPCHECK(hipMemcpyAsync(w_cent.p, cent, sizeof(float) * k * dd, hipMemcpyHostToDevice, stream));
       launch_row_norms(w_cent.as<float>(), k, dd, w_cn.as<float>(), stream);
       assign_top1(x, n, dd, w_cent.as<float>(), w_cn.as<float>(), k, assign.data(),
-                  resident ? xall.as<float>() : nullptr);
+                  resident ? xall.as<float>() : nullptr, ip_assign);
       kmeans_update(x, n, dd, k, assign.data(), cent);
     }
   }
 
   void upload_trained() {
+    quiesce();
     d_cent.ensure(sizeof(float) * nlist * d);
     d_cnorm.ensure(sizeof(float) * nlist);
     d_cb.ensure(sizeof(float) * M * ksub * (d / M));
@@ -337,6 +352,7 @@ struct ivfpq_index {
 
   void upload_lists() {
     if (!dirty) return;
+    quiesce();  // in-flight searches may still read the old device lists
     std::vector<int64_t> off(nlist + 1, 0);
     for (int l = 0; l < nlist; l++) off[l + 1] = off[l] + (int64_t)lids[l].size();
     const int64_t tot = off[nlist];
@@ -388,26 +404,31 @@ struct ivfpq_index {
     require(trained, "index is not trained");
     require(n >= 0, "n must be >= 0");
     require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]");
-    require(metric == IVFPQ_METRIC_L2, "only METRIC_L2 is served on the GPU");
   }
 
-  // coarse quantizer for c queries at x: nprobe nearest lists (fused kernel when
-  // the per-query distance rows fit in LDS, else distance matrix + select)
-  bool coarse_fused = true;  // IVFPQ_COARSE=split selects the two-kernel path (A/B)
-  // plan (nullable): list-major plan whose bucket counting the fused kernel may take over
-  void coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
-                     ListPlan* plan = nullptr) {
-    if (coarse_fused && nlist <= kCoarseFusedMax) {
-      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, plan,
-                          d_off.as<int64_t>(), list_lo, list_hi, plan ? w_T3.as<float>() : nullptr,
-                          d_cb.as<float>(), M);
-      return;
+  bool ip() const { return metric == IVFPQ_METRIC_INNER_PRODUCT; }
+
+  // Coarse quantizer for c queries at x: the nprobe best lists and the
+  // quantizer's values (L2 distances / IP similarities).  With `plan` (and
+  // nprobe <= 64, nlist within the fused kernel's LDS) the fused kernel also
+  // plans the batch and builds T3 and true is returned; otherwise the caller
+  // plans with launch_plan_count and builds T3 with launch_ip_table.
+  bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
+                     const ListPlan* plan = nullptr) {
+    if (coarse_fused_ok(nlist, np, d)) {
+      const bool planned = plan && np <= 64;
+      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, ip(),
+                          planned ? plan : nullptr, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>(),
+                          planned ? w_T3.as<float>() : nullptr, d_cb.as<float>(), M);
+      return planned;
     }
     w_xn.ensure(sizeof(float) * c);
     w_dist.ensure(sizeof(float) * c * nlist);
-    launch_row_norms(x, c, d, w_xn.as<float>(), s);
-    launch_l2_dist(x, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d, w_dist.as<float>(), s);
-    launch_select_rows(w_dist.as<float>(), c, nlist, np, dis, lists, s);
+    if (!ip()) launch_row_norms(x, c, d, w_xn.as<float>(), s);
+    launch_l2_dist(x, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d, w_dist.as<float>(), s,
+                   ip());
+    launch_select_rows(w_dist.as<float>(), c, nlist, np, dis, lists, s, ip());
+    return false;
   }
 
   // The full search on device pointers, on stream s.  Iq/Dq non-null = preassigned.
@@ -416,103 +437,80 @@ struct ivfpq_index {
     check_search(n, k);
     upload_lists();
     if (n == 0) return;
+    order_after_last(s);
     const int np = preassigned ? nprobe : eff_nprobe();
-    const size_t per_q = std::max<size_t>(std::max<size_t>((size_t)nlist, (size_t)M * ksub) * 4, (size_t)np * k * 48);
+    const int nloc = std::max(list_hi - list_lo, 1);
+    const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)np * k * 48, (size_t)nloc * 16});
     const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / per_q));
     w_T3.ensure(sizeof(float) * qc * M * ksub);
     if (!preassigned) {
-      w_xn.ensure(sizeof(float) * qc);
-      w_dist.ensure(sizeof(float) * qc * nlist);
       w_lists.ensure(sizeof(int64_t) * qc * np);
       w_dis0.ensure(sizeof(float) * qc * np);
     }
+    const int G = list_scan_group(M, k);
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
       const float* xq = x + q0 * d;
+      const ListPlan plan = make_plan(c, np, k, s);
       const int64_t* lists;
-      const float* dis0;
-      ListPlan plan;
-      if (!query_major) plan = make_plan(c, np, k);
+      bool planned = false;
+      const int tm = mark_begin(ST_COARSE, s);
       if (preassigned) {
         lists = Iq + q0 * np;
-        dis0 = Dq ? Dq + q0 * np : nullptr;
+        launch_plan_count(lists, (Dq && !ip()) ? Dq + q0 * np : nullptr, xq, d_cent.as<float>(), c, d, np,
+                          d_off.as<int64_t>(), list_lo, list_hi, ip(), true, k, plan, s);
       } else {
-        const int tm = mark_begin(ST_COARSE, s);
-        coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s,
-                      (query_major || (debug & 128)) ? nullptr : &plan);
-        mark_end(tm, s);
+        planned = coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s, &plan);
         lists = w_lists.as<int64_t>();
-        dis0 = w_dis0.as<float>();
+        if (!planned)
+          launch_plan_count(lists, ip() ? nullptr : w_dis0.as<float>(), xq, d_cent.as<float>(), c, d, np,
+                            d_off.as<int64_t>(), list_lo, list_hi, ip(), false, k, plan, s);
       }
-      // list-major with the seed pass: the seed launch builds T3 itself
-      const bool t3_in_seed = !query_major && !(debug & 64);
-      if (!t3_in_seed) {
+      mark_end(tm, s);
+      if (!planned) {
         const int tt = mark_begin(ST_TABLES, s);
         launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
         mark_end(tt, s);
       }
       ScanArgs a;
-      if (t3_in_seed && !plan.t3done) {
-        a.xq = xq;
-        a.cb = d_cb.as<float>();
-        a.d = d;
-        a.T3out = w_T3.as<float>();
-      }
       a.T1 = d_T1.as<float>();
       a.T3 = w_T3.as<float>();
       a.codes = d_codes.as<uint8_t>();
       a.ids = d_ids.as<int64_t>();
       a.list_off = d_off.as<int64_t>();
       a.probe_list = lists;
-      a.probe_dis0 = dis0;
       a.nq = c;
       a.nprobe = np;
       a.k = k;
       a.M = M;
+      a.ip = ip() ? 1 : 0;
       a.list_lo = list_lo;
       a.list_hi = list_hi;
-      a.debug = debug;
       a.outD = D + q0 * k;
       a.outI = I + q0 * k;
       const int ts = mark_begin(ST_SCAN, s);
-      if (query_major) {
-        launch_scan_topk(a, s);
-      } else {
-        const size_t sb = sizeof(uint64_t) * ((size_t)scan_lists_grid() * kStampItems * kStampSlots + (size_t)c * 4);
-        if (!stamp_out.empty()) {
-          w_stamps.ensure(sb);
-          HIPCHECK(hipMemsetAsync(w_stamps.p, 0, sb, s));
-          a.stamps = w_stamps.as<uint64_t>();
-        }
-        // ST_LISTS: its two events are re-recorded around the list-scan kernel alone
-        const int tl = mark_begin(ST_LISTS, s, false);
-        launch_scan_lists(a, plan, s, tl >= 0 ? &marks[tl].a : nullptr);
-        if (!stamp_out.empty()) {
-          std::vector<uint64_t> hs(sb / 8);
-          HIPCHECK(hipMemcpyAsync(hs.data(), w_stamps.p, sb, hipMemcpyDeviceToHost, s));
-          HIPCHECK(hipStreamSynchronize(s));
-          if (FILE* f = std::fopen(stamp_out.c_str(), "wb")) {
-            std::fwrite(hs.data(), 1, sb, f);
-            std::fclose(f);
-          }
-        }
-      }
+      launch_plan_items(plan, d_off.as<int64_t>(), list_lo, list_hi, G, s);
+      // ST_LISTS: its two events are recorded around the list-scan kernel alone
+      const int tl = mark_begin(ST_LISTS, s, false);
+      launch_scan_lists(a, plan, s, tl >= 0 ? &marks[tl].a : nullptr);
       mark_end(ts, s);
       HIPCHECK(hipGetLastError());
     }
+    mark_done(s);
   }
 
   void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {
     require(trained, "index is not trained");
+    if (n <= 0) return;
+    order_after_last(s);
     const int np = eff_nprobe();
     const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
-    w_xn.ensure(sizeof(float) * qc);
-    w_dist.ensure(sizeof(float) * qc * nlist);
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
       coarse_launch(x + q0 * d, c, np, Dq + q0 * np, Iq + q0 * np, s);
       HIPCHECK(hipGetLastError());
     }
+    mark_done(s);
   }
 
   // host-buffer search (copies in/out on the handle's stream)
@@ -520,6 +518,7 @@ struct ivfpq_index {
                    bool preassigned) {
     check_search(n, k);
     if (n == 0) return;
+    order_after_last(stream);
     const int np = nprobe;
     w_x.ensure(sizeof(float) * n * d);
     DevBuf dD, dI, dIq, dDq;
@@ -598,15 +597,6 @@ int ivfpq_create(int d, int nlist, int M, int nbits, int metric, int device, ivf
     h->list_hi = nlist;
     h->lcodes.resize(nlist);
     h->lids.resize(nlist);
-    const char* so = std::getenv("IVFPQ_STAMPS");
-    if (so) h->stamp_out = so;
-    const char* dbg = std::getenv("IVFPQ_DEBUG");
-    h->debug = dbg ? std::atoi(dbg) : 0;
-    if (h->debug & 48) set_coarse_debug((h->debug >> 4) & 3);
-    const char* cs = std::getenv("IVFPQ_COARSE");
-    h->coarse_fused = !(cs && std::string(cs) == "split");
-    const char* sc = std::getenv("IVFPQ_SCAN");
-    h->query_major = sc && std::string(sc) == "query";
     h->init_stream();
     *out = h.release();
   });
@@ -617,6 +607,7 @@ int ivfpq_free(ivfpq_index* h) {
     if (!h) return;
     DeviceGuard g(h->device);
     (void)hipStreamSynchronize(h->stream);
+    h->quiesce();
     delete h;
   });
 }
@@ -627,16 +618,17 @@ int ivfpq_train(ivfpq_index* h, int64_t n, const float* x, int niter_coarse, int
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     require(x != nullptr && n > 0, "empty training set");
+    h->quiesce();  // the k-means scratch buffers are shared with the search path
     const int d = h->d, M = h->M, dsub = d / M, ksub = h->ksub, nlist = h->nlist;
     std::vector<float> cent((size_t)nlist * d);
-    h->kmeans(x, n, d, nlist, niter_coarse, seed, cent.data());
+    h->kmeans(x, n, d, nlist, niter_coarse, seed, cent.data(), h->ip());
     // residuals to the final coarse centroids
     h->w_cent.ensure(sizeof(float) * nlist * d);
     h->w_cn.ensure(sizeof(float) * nlist);
     HIPCHECK(hipMemcpyAsync(h->w_cent.p, cent.data(), sizeof(float) * nlist * d, hipMemcpyHostToDevice, h->stream));
     launch_row_norms(h->w_cent.as<float>(), nlist, d, h->w_cn.as<float>(), h->stream);
     std::vector<int64_t> assign(n);
-    h->assign_top1(x, n, d, h->w_cent.as<float>(), h->w_cn.as<float>(), nlist, assign.data());
+    h->assign_top1(x, n, d, h->w_cent.as<float>(), h->w_cn.as<float>(), nlist, assign.data(), nullptr, h->ip());
     std::vector<float> sub((size_t)n * dsub);
     std::vector<float> cb((size_t)M * ksub * dsub);
     for (int m = 0; m < M; m++) {
@@ -673,6 +665,7 @@ int ivfpq_add(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids) {
     require(h->trained, "index is not trained");
     if (n <= 0) return;
     require(x != nullptr, "null x");
+    h->quiesce();  // the encode scratch buffers are shared with the search path
     const int d = h->d, M = h->M;
     const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)h->nlist * 4)));
     std::vector<int64_t> lno(rows);
@@ -687,9 +680,9 @@ int ivfpq_add(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids) {
     for (int64_t r0 = 0; r0 < n; r0 += rows) {
       const int64_t c = std::min(rows, n - r0);
       HIPCHECK(hipMemcpyAsync(h->w_x.p, x + r0 * d, sizeof(float) * c * d, hipMemcpyHostToDevice, h->stream));
-      launch_row_norms(h->w_x.as<float>(), c, d, h->w_xn.as<float>(), h->stream);
+      if (!h->ip()) launch_row_norms(h->w_x.as<float>(), c, d, h->w_xn.as<float>(), h->stream);
       launch_l2_dist(h->w_x.as<float>(), h->w_xn.as<float>(), c, h->d_cent.as<float>(), h->d_cnorm.as<float>(),
-                     h->nlist, d, h->w_dist.as<float>(), h->stream);
+                     h->nlist, d, h->w_dist.as<float>(), h->stream, h->ip());
       launch_select_rows(h->w_dist.as<float>(), c, h->nlist, 1, h->w_D.as<float>(), h->w_lno.as<int64_t>(),
                          h->stream);
       launch_pq_encode(h->w_x.as<float>(), c, d, h->d_cent.as<float>(), h->w_lno.as<int64_t>(),
@@ -814,11 +807,12 @@ int ivfpq_coarse_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, 
   });
 }
 
-int ivfpq_merge_topk_device(int S, int64_t n, int k, const float* Din, const int64_t* Iin, float* Dout,
+int ivfpq_merge_topk_device(int S, int64_t n, int k, int metric, const float* Din, const int64_t* Iin, float* Dout,
                             int64_t* Iout, void* stream) {
   return guarded([&] {
-    require(S >= 1 && k >= 1, "invalid merge shape");
-    launch_merge_topk(S, n, k, Din, Iin, Dout, Iout, (hipStream_t)stream);
+    require(S >= 1 && k >= 1 && n >= 0, "invalid merge shape");
+    require(metric == IVFPQ_METRIC_L2 || metric == IVFPQ_METRIC_INNER_PRODUCT, "unknown metric");
+    launch_merge_topk(S, n, k, Din, Iin, Dout, Iout, (hipStream_t)stream, metric == IVFPQ_METRIC_INNER_PRODUCT);
     HIPCHECK(hipGetLastError());
   });
 }
@@ -986,10 +980,12 @@ int ivfpq_load(const char* path, int device, ivfpq_index** out) {
   return rc;
 }
 
-int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n, const float* x, int k, float* D,
-                      int64_t* I) {
+int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n, const float* x, int k, int metric,
+                      float* D, int64_t* I) {
   return guarded([&] {
     require(d > 0 && nb >= 0 && n >= 0, "invalid shape");
+    require(metric == IVFPQ_METRIC_L2 || metric == IVFPQ_METRIC_INNER_PRODUCT, "unknown metric");
+    const bool ip = metric == IVFPQ_METRIC_INNER_PRODUCT;
     require(k >= 1 && k <= kMaxK, "k must be in [1, " + std::to_string(kMaxK) + "]");
     if (n == 0) return;
     DeviceGuard g(device);
@@ -1013,8 +1009,8 @@ int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n,
       HIPCHECK(hipMemcpyAsync(dx.p, x + q0 * d, sizeof(float) * c * d, hipMemcpyHostToDevice, s));
       launch_row_norms(dx.as<float>(), c, d, dxn.as<float>(), s);
       launch_l2_dist(dx.as<float>(), dxn.as<float>(), c, dxb.as<float>(), dbn.as<float>(), (int)nb, d,
-                     ddist.as<float>(), s);
-      launch_select_rows(ddist.as<float>(), c, (int)nb, k, dD.as<float>(), dI.as<int64_t>(), s);
+                     ddist.as<float>(), s, ip);
+      launch_select_rows(ddist.as<float>(), c, (int)nb, k, dD.as<float>(), dI.as<int64_t>(), s, ip);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipMemcpyAsync(D + q0 * k, dD.p, sizeof(float) * c * k, hipMemcpyDeviceToHost, s));
       HIPCHECK(hipMemcpyAsync(I + q0 * k, dI.p, sizeof(int64_t) * c * k, hipMemcpyDeviceToHost, s));

@@ -7,19 +7,25 @@
 // classify_stages.py:127-136) and on the FPGA (retrieval_accelerator/
 // entire_accelerator_final_SIFT_M16/src/{LUT_construction,ADC}.hpp).
 //
-// Design:
-//  * one 256-thread workgroup per query; the query's inner-product table T3
-//    (M x 256 fp32) is held in VGPRs; for every probed list the workgroup
-//    forms LUT = T1[list] + (-2) T3 directly in LDS (the LUT never touches
-//    HBM), then the four waves stream the list's PQ codes (16 B per lane,
-//    coalesced 1 KiB per wave-instruction) and sum M LDS lookups per code;
-//  * top-k is fused into the scan: each wave keeps its k best (dist, label)
-//    pairs sorted across lanes in registers (R = ceil(k/64) rows) and admits a
-//    candidate only if it beats the wave's current k-th; the four wave lists
-//    are merged by rank at the end.  No distance is ever written to memory.
-//  * every fp32 operation follows the oracle's order (oracle/ivfpq_oracle.c,
-//    Faiss 1.7.1 AVX order); the library is compiled with -ffp-contract=off
-//    and the only FMAs are the explicit fmaf() of the coarse inner product.
+// Design, four launches per batch:
+//  * k_coarse_fused: per query the nprobe nearest lists (fmaf-chain inner
+//    products, wave-level selection), its T3 table, and in the epilogue the
+//    list-major plan: every (query, probe) pair is bucketed under its list,
+//    the query's first usable probe as kind 0, the others as kind 1;
+//  * k_plan_items: (list, up to G pairs) work item records, kind 0 first;
+//  * k_scan_lists: persistent workgroups; per item the G LUTs
+//    (T1[list] - 2 T3[q], or -T3[q] for IP) are formed in LDS (the LUT never
+//    touches HBM) from rows prefetched into registers during the previous
+//    item, the list's PQ codes are streamed coalesced and every code is summed
+//    from M LDS lookups per query; top-k is fused into the scan (per-wave
+//    candidate queue + DPP wave top-k in registers, admission against the
+//    query's running k-th key shared through atomicMin), so no distance is
+//    ever written to memory;
+//  * k_merge_probes: per query the per-wave partial lists of its probes,
+//    labels looked up for survivors only.
+// Every fp32 operation follows the oracle's order (oracle/ivfpq_oracle.c,
+// Faiss 1.7.1 AVX order); the library is compiled with -ffp-contract=off and
+// the only FMAs are the explicit fmaf() of the coarse inner product.
 #include <float.h>
 #include <stdint.h>
 
@@ -406,6 +412,14 @@ __device__ __forceinline__ bool wave_select_threshold(const float (&d)[16], cons
   return true;
 }
 
+// order-preserving int image of a float (signed int compare == float compare),
+// for atomicMin on keys that may be negative (IP keys, rounding-negative L2)
+__device__ __forceinline__ int f2ord(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ord2f(int o) { return __int_as_float(o >= 0 ? o : o ^ 0x7FFFFFFF); }
+
 // ------------------------------------------------------------------ norms
 __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int d,
                                                    float* __restrict__ out) {
@@ -415,7 +429,7 @@ __global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, 
   out[i] = tree<K_NORM>([&](int t) { return xi[t]; }, [&](int t) { return xi[t]; }, d);
 }
 
-// ------------------------------------------------- coarse L2 distance matrix
+// ------------------------------------------------- coarse key matrix (split path)
 // 64 x 64 output tile per 256-thread workgroup, 4 x 4 per thread, K staged in
 // LDS 16 at a time.  Each output's inner product is a k-ordered fmaf chain.
 constexpr int DT_B = 64;
@@ -424,7 +438,7 @@ constexpr int DT_K = 16;
 __global__ __launch_bounds__(256) void k_l2_dist(const float* __restrict__ x, const float* __restrict__ xn,
                                                  int64_t nx, const float* __restrict__ c,
                                                  const float* __restrict__ cn, int nc, int d,
-                                                 float* __restrict__ out) {
+                                                 float* __restrict__ out, int ip) {
   __shared__ float xs[DT_K][DT_B + 4];
   __shared__ float cs[DT_K][DT_B + 4];
   const int tid = threadIdx.x;
@@ -449,15 +463,15 @@ __global__ __launch_bounds__(256) void k_l2_dist(const float* __restrict__ x, co
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < DT_K; kk++) {
-      float a[4], b[4];
+      float av[4], bv[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) a[i] = xs[kk][ty * 4 + i];
+      for (int i = 0; i < 4; i++) av[i] = xs[kk][ty * 4 + i];
 #pragma unroll
-      for (int j = 0; j < 4; j++) b[j] = cs[kk][tx * 4 + j];
+      for (int j = 0; j < 4; j++) bv[j] = cs[kk][tx * 4 + j];
 #pragma unroll
       for (int i = 0; i < 4; i++)
 #pragma unroll
-        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_fmaf(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 4; j++) acc[i][j] = __builtin_fmaf(av[i], bv[j], acc[i][j]);
     }
     __syncthreads();
   }
@@ -465,46 +479,57 @@ __global__ __launch_bounds__(256) void k_l2_dist(const float* __restrict__ x, co
   for (int i = 0; i < 4; i++) {
     const int64_t r = row0 + ty * 4 + i;
     if (r >= nx) continue;
-    const float xr = xn[r];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       const int64_t cc = col0 + tx * 4 + j;
       if (cc >= nc) continue;
-      float dis = (xr + cn[cc]) - 2.0f * acc[i][j];
-      if (dis < 0.f) dis = 0.f;
+      float dis;
+      if (ip) {
+        dis = -acc[i][j];
+      } else {
+        dis = (xn[r] + cn[cc]) - 2.0f * acc[i][j];
+        if (dis < 0.f) dis = 0.f;
+      }
       out[r * nc + cc] = dis;
     }
   }
+}
+
+// ---------------------------------------------------------- planning helpers
+// One (query, probe) pair of a batch: kind 0 when it is the query's first
+// usable probe, else kind 1; bucketed under its list with the scan's dis0.
+__device__ __forceinline__ void plan_pair(const ListPlan& pl, int nloc, int64_t l, int lo, int kind, int pair,
+                                          float dis0) {
+  const int s = atomicAdd(&pl.cnt[kind * nloc + (int)(l - lo)], 1);
+  // a list holds at most one pair per query and kind, so s < cap (deduplicated rows)
+  if (s < pl.cap) pl.bucket[((int64_t)(l - lo) * 2 + kind) * pl.cap + s] = make_int2(pair, __float_as_int(dis0));
 }
 
 // ------------------------------------------------------- fused coarse probe
 // 4 queries per 256-thread workgroup.  Thread t owns centroids 4t..4t+3 of each
 // 1024-centroid block (float4 loads of the transposed centroids, coalesced) and
 // accumulates <x_q, c> as a k-ordered fmaf chain for the 4 queries (query
-// elements broadcast from LDS).  Distances land in LDS; wave w then selects
-// query w's nprobe nearest lists (same rule and arithmetic as k_l2_dist +
+// elements broadcast from LDS).  Keys land in LDS; wave w then selects
+// query w's nprobe smallest (same rule and arithmetic as k_l2_dist +
 // k_select_rows).
 constexpr int CQ = 4;
-__device__ int g_coarse_debug = 0;
 
-// Optional list-major planning folded into the coarse epilogue (nprobe <= 64):
-// per query the first usable probe, tau_q reset and the per-list pair counts
-// of k_first_probe + k_bucket_count.
 struct CoarsePlan {
-  const int64_t* list_off = nullptr;  // null: no planning
-  int lo = 0, hi = 0;
   ListPlan pl;
-  // also T3 for the workgroup's queries (k_ip_table's tree; the codebook is read once per 4 queries)
-  float* T3out = nullptr;
+  int on = 0;                         // 0: no planning (nprobe > 64, or not requested)
+  const int64_t* list_off = nullptr;
+  int lo = 0, hi = 0;
+  const float* cent = nullptr;        // [nlist][d] row-major (IP dis0)
+  float* T3out = nullptr;             // [nq][M][256] (null: no T3)
   const float* cb = nullptr;
   int M = 0;
-};  // 1: skip the distance loop, 2: skip the selection (timing only)
+};
 
 template <int R>
 __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
                                                       const float* __restrict__ centT, const float* __restrict__ cn,
                                                       int nlist, int nprobe, float* __restrict__ out_dis,
-                                                      int64_t* __restrict__ out_list, CoarsePlan cp) {
+                                                      int64_t* __restrict__ out_list, int ip, CoarsePlan cp) {
   extern __shared__ __attribute__((aligned(16))) float cs_mem[];
   float* xs = cs_mem;                       // [CQ][d]
   float* xn = xs + CQ * d;                  // [CQ]
@@ -569,7 +594,7 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
     for (int qq = 0; qq < CQ; qq++)
 #pragma unroll
       for (int u = 0; u < 4; u++) acc[qq][u] = 0.f;
-    if (c4 < nlist && !(g_coarse_debug & 1)) {
+    if (c4 < nlist) {
       // centT rows are padded to a multiple of 4 columns: branch-free float4 loads
       const int ldc = (nlist + 3) & ~3;
       constexpr int KB = 16;  // centroid rows in flight
@@ -600,11 +625,16 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
     for (int u = 0; u < 4; u++) {
       const int c = c4 + u;
       if (c < nlist) {
-        const float cnv = cn[c];
+        const float cnv = ip ? 0.f : cn[c];
 #pragma unroll
         for (int qq = 0; qq < CQ; qq++) {
-          float dis = (xn[qq] + cnv) - 2.0f * acc[qq][u];
-          if (dis < 0.f) dis = 0.f;
+          float dis;
+          if (ip) {
+            dis = -acc[qq][u];
+          } else {
+            dis = (xn[qq] + cnv) - 2.0f * acc[qq][u];
+            if (dis < 0.f) dis = 0.f;
+          }
           dist[qq * nlist + c] = dis;
         }
       }
@@ -613,16 +643,8 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
   __syncthreads();
   const int64_t q = q0 + wave;
   if (q >= nq) return;
-  WaveTopK<R> tk;
-  tk.init(nprobe);
+  const float pad = ip ? -FLT_MAX : FLT_MAX;
   float* drow = dist + wave * nlist;  // LDS row of this wave's query
-  if (g_coarse_debug & 2) {
-    if (lane < nprobe) {
-      out_dis[q * nprobe + lane] = drow[lane];
-      out_list[q * nprobe + lane] = lane;
-    }
-    return;
-  }
   if constexpr (R == 1) {
     // 16 candidates per lane per 1024-centroid block: sort in registers, 64-way
     // merge for the block's nprobe best, fold into the running list
@@ -659,23 +681,29 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
     }
     if (lane < nprobe) {
       const bool empty = ri == kSentinelId;
-      out_dis[q * nprobe + lane] = empty ? FLT_MAX : rd;
+      out_dis[q * nprobe + lane] = empty ? pad : (ip ? -rd : rd);
       out_list[q * nprobe + lane] = empty ? -1 : ri;
     }
-    if (cp.list_off) {  // same rules as k_first_probe + k_bucket_count
+    if (cp.on) {  // list-major planning of this query's probes (k_plan_count's rules)
       const int64_t l = ri;  // kSentinelId when empty: outside [lo, hi)
       const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
       const uint64_t um = __ballot(use);
-      const int fp = (cp.pl.seed && um) ? (int)__builtin_ctzll(um) : nprobe;
-      if (lane == 0) {
-        cp.pl.first_probe[q] = fp;
-        cp.pl.tauq[q] = __float_as_int(kInf);
+      const int fp = um ? (int)__builtin_ctzll(um) : 64;
+      if (lane == 0) cp.pl.tauq[q] = f2ord(kInf);
+      if (use) {
+        float d0 = rd;
+        if (ip) {
+          const float* xq = xs + wave * d;
+          const float* cl = cp.cent + l * d;
+          d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
+        }
+        plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
       }
-      if (lane < nprobe)
-        cp.pl.slot[q * nprobe + lane] = (use && lane != fp) ? atomicAdd(&cp.pl.cnt[(int)(l - cp.lo)], 1) : -1;
     }
     return;
   }
+  WaveTopK<R> tk;
+  tk.init(nprobe);
   for (int base = 0; base < nlist; base += 64) {
     const int cix = base + lane;
     const bool valid = cix < nlist;
@@ -690,7 +718,7 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
     const int idx = r * 64 + lane;
     if (idx < nprobe) {
       const bool empty = tk.id[r] == kSentinelId;
-      out_dis[q * nprobe + idx] = empty ? FLT_MAX : tk.d[r];
+      out_dis[q * nprobe + idx] = empty ? pad : (ip ? -tk.d[r] : tk.d[r]);
       out_list[q * nprobe + idx] = empty ? -1 : tk.id[r];
     }
   }
@@ -699,7 +727,8 @@ __global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ 
 // ------------------------------------------------------------ row select
 template <int R>
 __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ dist, int64_t nrows, int ncols,
-                                                     int n, float* __restrict__ ov, int64_t* __restrict__ oc) {
+                                                     int n, float* __restrict__ ov, int64_t* __restrict__ oc,
+                                                     int neg) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= nrows) return;  // wave-uniform
@@ -721,12 +750,13 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
     }
     tk.insert(mask, v, (int64_t)cix, lane);
   }
+  const float pad = neg ? -FLT_MAX : FLT_MAX;
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const int idx = r * 64 + lane;
     if (idx < n) {
       const bool empty = tk.id[r] == kSentinelId;
-      ov[row * n + idx] = empty ? FLT_MAX : tk.d[r];
+      ov[row * n + idx] = empty ? pad : (neg ? -tk.d[r] : tk.d[r]);
       oc[row * n + idx] = empty ? -1 : tk.id[r];
     }
   }
@@ -735,8 +765,7 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
 // -------------------------------------------------------------- PQ tables
 // T3, one workgroup per query: thread t computes entries [16t, 16t+16) of the
 // query's M x 256 table (m = t / 16); q is staged in LDS, codebook rows are
-// contiguous, the 64-B output per thread is stored as 4 x float4.  DSUB = 0 is
-// the generic (runtime dsub) variant.
+// contiguous.  DSUB = 0 is the generic (runtime dsub) variant.
 template <int DSUB>
 __global__ __launch_bounds__(256) void k_ip_table(const float* __restrict__ x, int64_t n, int d,
                                                   const float* __restrict__ cb, int M, int ksub,
@@ -822,7 +851,201 @@ __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ x, 
   codes[gid] = (uint8_t)best;
 }
 
-// ------------------------------------------------------- fused scan + top-k
+// ===================================================== list-major planning
+// One wave per query: tau reset, first usable probe, per-list pair counts and
+// bucket entries (the fused coarse epilogue does the same for its batch).
+// dedup (caller-supplied rows): a list repeated in a query's row is scanned
+// once, at its first position; the later pairs are reported as empty partials.
+__global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ lists, const float* __restrict__ Dq,
+                                                    const float* __restrict__ x, const float* __restrict__ cent,
+                                                    int64_t nq, int d, int nprobe,
+                                                    const int64_t* __restrict__ list_off, int lo, int hi, int ip,
+                                                    int dedup, int k, ListPlan pl) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  if (lane == 0) pl.tauq[q] = f2ord(kInf);
+  bool found = false;
+  for (int p0 = 0; p0 < nprobe; p0 += 64) {
+    const int p = p0 + lane;
+    const int64_t l = p < nprobe ? lists[q * nprobe + p] : -1;
+    bool use = p < nprobe && l >= lo && l < hi && list_off[l + 1] > list_off[l];
+    if (dedup && use) {
+      bool dup = false;
+      for (int j = 0; j < p && !dup; j++) dup = lists[q * nprobe + j] == l;
+      if (dup) {  // the merge reads every usable pair's partial slots: write them empty
+        use = false;
+        const int64_t o = (q * nprobe + p) * 4 * (int64_t)k;
+        for (int e = 0; e < 4 * k; e++) {
+          pl.partD[o + e] = FLT_MAX;
+          pl.partI[o + e] = -1;
+        }
+      }
+    }
+    const uint64_t um = __ballot(use);
+    const int fp = (!found && um) ? (int)__builtin_ctzll(um) : 64;
+    found = found || um != 0;
+    if (use) {
+      float d0;
+      if (ip) {
+        const float* xq = x + q * d;
+        const float* cl = cent + l * d;
+        d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
+      } else {
+        d0 = Dq ? Dq[q * nprobe + p] : 0.f;
+      }
+      plan_pair(pl, hi - lo, l, lo, lane == fp ? 0 : 1, (int)(q * nprobe + p), d0);
+    }
+  }
+}
+
+// Work items from the per-list counts.  Every workgroup re-derives the item
+// offsets of the lists before its own 1024 (a reduction over the counts), scans
+// its own lists' item counts in LDS, and writes the records of its items, one
+// item per thread.  Items of kind 0 occupy [0, N0), kind 1 [N0, N0 + N1).
+constexpr int PLAN_T = 1024;
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int o = __shfl_up(v, off, 64);
+    if (lane >= off) v += o;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(PLAN_T) void k_plan_items(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
+                                                       int nloc, int G) {
+  __shared__ int red[4][PLAN_T / 64];
+  __shared__ int ex0[PLAN_T + 1], ex1[PLAN_T + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = PLAN_T / 64;
+  const int my0 = blockIdx.x * PLAN_T;
+  int t0 = 0, t1 = 0, p0 = 0, p1 = 0;
+  for (int j = tid; j < nloc; j += PLAN_T) {
+    const int a = (min(pl.cnt[j], pl.cap) + G - 1) / G, b = (min(pl.cnt[nloc + j], pl.cap) + G - 1) / G;
+    t0 += a;
+    t1 += b;
+    if (j < my0) {
+      p0 += a;
+      p1 += b;
+    }
+  }
+  t0 = wave_incl_scan(t0, lane);
+  t1 = wave_incl_scan(t1, lane);
+  p0 = wave_incl_scan(p0, lane);
+  p1 = wave_incl_scan(p1, lane);
+  if (lane == 63) {
+    red[0][wave] = t0;
+    red[1][wave] = t1;
+    red[2][wave] = p0;
+    red[3][wave] = p1;
+  }
+  // own lists: item counts and their exclusive scan
+  const int j = my0 + tid;
+  const int a = j < nloc ? (min(pl.cnt[j], pl.cap) + G - 1) / G : 0;
+  const int b = j < nloc ? (min(pl.cnt[nloc + j], pl.cap) + G - 1) / G : 0;
+  const int ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane);
+  __shared__ int wsa[NW], wsb[NW];
+  if (lane == 63) {
+    wsa[wave] = ia;
+    wsb[wave] = ib;
+  }
+  __syncthreads();
+  int T0 = 0, T1 = 0, P0 = 0, P1 = 0, ba = 0, bb = 0;
+  for (int w = 0; w < NW; w++) {
+    T0 += red[0][w];
+    T1 += red[1][w];
+    P0 += red[2][w];
+    P1 += red[3][w];
+    if (w < wave) {
+      ba += wsa[w];
+      bb += wsb[w];
+    }
+  }
+  ex0[tid + 1] = ba + ia;
+  ex1[tid + 1] = bb + ib;
+  if (tid == 0) {
+    ex0[0] = 0;
+    ex1[0] = 0;
+  }
+  if (blockIdx.x == 0 && tid < 16) pl.hdr[tid] = tid == 0 ? T0 + T1 : tid == 1 ? T0 : 0;
+  __syncthreads();
+  const int own0 = ex0[PLAN_T], own1 = ex1[PLAN_T];
+  for (int e = tid; e < own0 + own1; e += PLAN_T) {
+    const int kind = e < own0 ? 0 : 1;
+    const int ek = kind ? e - own0 : e;
+    const int* ex = kind ? ex1 : ex0;
+    int lo_i = 0, hi_i = PLAN_T;  // largest jl with ex[jl] <= ek
+    while (hi_i - lo_i > 1) {
+      const int mid = (lo_i + hi_i) >> 1;
+      if (ex[mid] <= ek)
+        lo_i = mid;
+      else
+        hi_i = mid;
+    }
+    const int jl = lo_i;
+    const int t = ek - ex[jl];
+    const int jj = my0 + jl;
+    const int c = min(pl.cnt[kind * nloc + jj], pl.cap);
+    const int cnt = min(G, c - t * G);
+    const int64_t l = lo + jj;
+    const int64_t beg = list_off[l];
+    const int rec = kind ? T0 + P1 + ek : P0 + ek;
+    int r[16];
+    r[0] = (int)l;
+    r[1] = cnt;
+    r[2] = (int)(list_off[l + 1] - beg);
+    r[3] = (int)(uint32_t)(uint64_t)beg;
+    r[4] = (int)(uint32_t)((uint64_t)beg >> 32);
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      int2 v = make_int2(0, 0);
+      if (g < cnt) {
+        const int s = t * G + g;
+        v = pl.bucket[((int64_t)jj * 2 + kind) * pl.cap + s];
+      }
+      r[5 + g] = v.x;
+      r[9 + g] = v.y;
+    }
+    r[13] = kind;
+    r[14] = 0;
+    r[15] = 0;
+    int4* rp = reinterpret_cast<int4*>(pl.recs + (int64_t)rec * 16);
+    rp[0] = make_int4(r[0], r[1], r[2], r[3]);
+    rp[1] = make_int4(r[4], r[5], r[6], r[7]);
+    rp[2] = make_int4(r[8], r[9], r[10], r[11]);
+    rp[3] = make_int4(r[12], r[13], r[14], r[15]);
+  }
+}
+
+// ===================================================== list scan (phase B)
+template <int G>
+struct LutVec;
+template <>
+struct LutVec<1> {
+  using T = float;
+};
+template <>
+struct LutVec<2> {
+  using T = float2;
+};
+template <>
+struct LutVec<4> {
+  using T = float4;
+};
+
+__device__ __forceinline__ float comp(float v, int) { return v; }
+__device__ __forceinline__ float comp(float2 v, int g) { return g == 0 ? v.x : v.y; }
+__device__ __forceinline__ float comp(float4 v, int g) { return g == 0 ? v.x : g == 1 ? v.y : g == 2 ? v.z : v.w; }
+__device__ __forceinline__ void setc(float& o, int, float x) { o = x; }
+__device__ __forceinline__ void setc(float2& o, int g, float x) {
+  if (g == 0) o.x = x; else o.y = x;
+}
+__device__ __forceinline__ void setc(float4& o, int g, float x) {
+  if (g == 0) o.x = x; else if (g == 1) o.y = x; else if (g == 2) o.z = x; else o.w = x;
+}
+
 template <int M>
 struct CodeWords {
   uint32_t w[M / 4];
@@ -851,476 +1074,179 @@ struct CodeWords {
   __device__ __forceinline__ uint32_t byte(int m) const { return (w[m >> 2] >> ((m & 3) * 8)) & 0xffu; }
 };
 
-// POSKEY: rank candidates by (distance, global code position) and translate
-// positions to labels only for the k survivors.  Valid when all candidates
-// come from ONE inverted list (seed mode): the device image of every list is
-// sorted by label, so position order equals label order inside a list.
-template <int M, int R, bool POSKEY>
-__global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
-  constexpr int LUTN = M * 256;  // fp32 entries per LUT
-  constexpr int NV4 = M / 4;     // float4 per thread while forming the LUT
-  constexpr int KP = R * 64;
-  constexpr int LUT_BYTES = LUTN * 4;
-  constexpr int MERGE_BYTES = 4 * KP * 12;
-  constexpr int SMEM = LUT_BYTES > MERGE_BYTES ? LUT_BYTES : MERGE_BYTES;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
-  float* lut = reinterpret_cast<float*>(smem);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int64_t q = blockIdx.x;
-  const int k = a.k;
-  if (a.scat_recs) {
-    // seed launch with the bucket scatter folded in (replaces k_bucket_scatter):
-    // this query's non-seed pairs go into their work item records
-    for (int p = tid; p < a.nprobe; p += 256) {
-      const int64_t i = q * a.nprobe + p;
-      const int sl = a.scat_slot[i];
-      if (sl < 0) continue;
-      const int G = a.scat_G;
-      int32_t* r = a.scat_recs + (int64_t)(a.scat_ioff[(int)(a.probe_list[i] - a.list_lo)] + sl / G) * 16;
-      r[5 + sl % G] = (int32_t)i;
-      r[9 + sl % G] = __float_as_int(a.probe_dis0 ? a.probe_dis0[i] : 0.f);
-    }
-  }
-  // diagnostic stamps (seed mode): [q][4] = start, LUT ready, scan done, end
-  auto qstamp = [&](int slot) {
-    if (a.stamps && threadIdx.x == 0) a.stamps[q * 4 + slot] = __builtin_amdgcn_s_memtime();
-  };
-  qstamp(0);
-
-  // This thread's slice of the query's T3 (float4 index e*256 + tid).
-  float4 t3[NV4];
-  if (a.T3out) {
-    // seed mode with the table build folded in (replaces k_ip_table): entries
-    // 4(e*256+tid)+c, same k_ip_table tree, stored for the list scan
-    float* xs = lut;  // the query, staged in the (not yet used) LUT space; d <= M * 256
-    for (int e = tid; e < a.d; e += 256) xs[e] = a.xq[q * a.d + e];
-    __syncthreads();
-    const int dsub = a.d / M;
-#pragma unroll
-    for (int e = 0; e < NV4; e++) {
-      const int e4 = 4 * (e * 256 + tid);
-      const float* xm = xs + (e4 >> 8) * dsub;  // the 4 entries share m (256 per m)
-      float v[4];
-      if (dsub == 8) {
-        const float4* src = reinterpret_cast<const float4*>(a.cb + (int64_t)e4 * 8);
-        float4 cw[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) cw[u] = src[u];
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const float* w = reinterpret_cast<const float*>(&cw[2 * c]);
-          v[c] = tree<K_IP>([&](int t) { return xm[t]; }, [&](int t) { return w[t]; }, 8);
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const float* w = a.cb + (int64_t)(e4 + c) * dsub;
-          v[c] = tree<K_IP>([&](int t) { return xm[t]; }, [&](int t) { return w[t]; }, dsub);
-        }
-      }
-      t3[e] = make_float4(v[0], v[1], v[2], v[3]);
-      reinterpret_cast<float4*>(a.T3out + q * LUTN)[e * 256 + tid] = t3[e];
-    }
-    // the LUT build below overwrites xs only after the loop's first barrier
-  } else {
-    const float4* T3q = reinterpret_cast<const float4*>(a.T3 + q * LUTN);
-#pragma unroll
-    for (int e = 0; e < NV4; e++) t3[e] = T3q[e * 256 + tid];
-  }
-
-  WaveTopK<R> tk;
-  tk.init(k);
-
-  int p_begin = 0, p_end = a.nprobe;
-  qstamp(2);
-  if (a.first_probe) {  // threshold-seed mode: only the first usable probe
-    p_begin = a.first_probe[q];
-    p_end = min(p_begin + 1, a.nprobe);
-  }
-  for (int p = p_begin; p < p_end; ++p) {
-    const int64_t l = a.probe_list[q * a.nprobe + p];
-    if (l < a.list_lo || l >= a.list_hi) continue;  // skipped probe (-1) or another shard's list
-    const float d0 = a.probe_dis0 ? a.probe_dis0[q * a.nprobe + p] : 0.f;
-
-    __syncthreads();  // every wave is done with the previous LUT
-    {
-      const float4* T1l = reinterpret_cast<const float4*>(a.T1 + l * LUTN);
-      float4* lut4 = reinterpret_cast<float4*>(lut);
-#pragma unroll
-      for (int e = 0; e < NV4; e++) {
-        float4 v = T1l[e * 256 + tid];
-        const float4 t = t3[e];
-        v.x = v.x + (-2.0f * t.x);
-        v.y = v.y + (-2.0f * t.y);
-        v.z = v.z + (-2.0f * t.z);
-        v.w = v.w + (-2.0f * t.w);
-        lut4[e * 256 + tid] = v;
-      }
-    }
-    __syncthreads();
-
-    qstamp(1);
-    const int64_t beg = a.list_off[l];
-    const int64_t n = a.list_off[l + 1] - beg;
-    const uint8_t* lc = a.codes + beg * M;
-    const int64_t* lid = a.ids + beg;
-    constexpr int JQ = M <= 16 ? 4 : 2;  // codes per lane per round trip
-    for (int64_t base = wave * 64; base < n; base += 256 * JQ) {
-      CodeWords<M> cw[JQ];
-#pragma unroll
-      for (int j = 0; j < JQ; j++) {
-        const int64_t i = base + j * 256 + lane;
-        cw[j].load(lc + (i < n ? i : 0) * M);  // clamped: branch-free batch of loads
-      }
-      float dj[JQ];  // m-outer: JQ independent gathers in flight, no branches between
-#pragma unroll
-      for (int j = 0; j < JQ; j++) dj[j] = d0;
-#pragma unroll
-      for (int m = 0; m < M; m++)
-#pragma unroll
-        for (int j = 0; j < JQ; j++) dj[j] = dj[j] + lut[m * 256 + cw[j].byte(m)];
-#pragma unroll
-      for (int j = 0; j < JQ; j++) {
-        const int64_t i = base + j * 256 + lane;
-        const bool valid = i < n;
-        const float dis = dj[j];
-        const bool maybe = valid && dis <= tk.td;
-        int64_t id = kSentinelId;
-        if constexpr (POSKEY) {
-          id = beg + i;
-        } else {
-          if (maybe) id = lid[i];
-        }
-        const bool pass = maybe && lexless(dis, id, tk.td, tk.ti);
-        const uint64_t mask = __ballot(pass);
-        if (mask) {
-          if constexpr (R == 1) {
-            if (__popcll(mask) > 6)
-              bulk_merge_row(tk, pass ? dis : kInf, pass ? id : kSentinelId, lane);
-            else
-              tk.insert(mask, dis, id, lane);
-          } else {
-            tk.insert(mask, dis, id, lane);
-          }
-        }
-      }
-    }
-  }
-
-  if (a.first_probe) {
-    // seed mode: every wave writes its own sorted list; any wave's k-th bounds
-    // the query's final k-th (phase B admission)
-    if (p_begin >= a.nprobe) return;
-    const int64_t o = ((q * a.nprobe + p_begin) * 4 + wave) * k;
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int idx = r * 64 + lane;
-      if (idx < k) {
-        const bool empty = tk.id[r] == kSentinelId;
-        a.partD[o + idx] = empty ? FLT_MAX : tk.d[r];
-        a.partI[o + idx] = empty ? -1 : tk.id[r];
-      }
-    }
-    qstamp(3);
-    if (lane == 0 && tk.td < kInf) atomicMin(&a.tauq[q], __float_as_int(tk.td));
-    return;
-  }
-  // ---- merge the four wave lists by rank
-  __syncthreads();
-  float* md = reinterpret_cast<float*>(smem);
-  int64_t* mi = reinterpret_cast<int64_t*>(smem + 4 * KP * 4);
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int idx = r * 64 + lane;
-    if (idx < k) {
-      md[wave * KP + idx] = tk.d[r];
-      mi[wave * KP + idx] = tk.id[r];
-    }
-  }
-  __syncthreads();
-  for (int e = tid; e < 4 * k; e += 256) {
-    const int w = e / k;
-    const int idx = e - w * k;
-    const float vd = md[w * KP + idx];
-    const int64_t vi = mi[w * KP + idx];
-    int rank = idx;
-#pragma unroll
-    for (int w2 = 0; w2 < 4; w2++) {
-      if (w2 == w) continue;
-      int lo = 0, hi = k;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const float ed = md[w2 * KP + mid];
-        const int64_t ei = mi[w2 * KP + mid];
-        const bool before = (w2 < w) ? !lexless(vd, vi, ed, ei) : lexless(ed, ei, vd, vi);
-        if (before)
-          lo = mid + 1;
-        else
-          hi = mid;
-      }
-      rank += lo;
-    }
-    if (rank < k) {
-      const bool empty = vi == kSentinelId;
-      a.outD[q * k + rank] = empty ? FLT_MAX : vd;
-      a.outI[q * k + rank] = empty ? -1 : (POSKEY ? a.ids[vi] : vi);
-    }
-  }
-}
-
-
-// ===================================================== list-major two-phase scan
-// Bucketing: pairs (q, p) whose list is in the shard range and non-empty are
-// counted per list (global atomics), a single workgroup scans the counts into
-// bucket offsets and (list, bucket offset, count<=G) work items, then the pair
-// ids are scattered.  Order inside a bucket is arbitrary: results do not depend
-// on it (each (query, code) distance is computed independently and the final
-// order is (distance, label)).
-constexpr int PLAN_T = 1024;
-
-__device__ __forceinline__ bool usable_list(int64_t l, int lo, int hi, const int64_t* list_off) {
-  return l >= lo && l < hi && list_off[l + 1] > list_off[l];
-}
-
-// first usable probe per query (nprobe if none); also zeroes the per-list counters
-__global__ __launch_bounds__(256) void k_first_probe(const int64_t* __restrict__ lists, int64_t nq, int nprobe,
-                                                     const int64_t* __restrict__ list_off, int lo, int hi,
-                                                     ListPlan pl) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t < (int64_t)(hi - lo)) pl.cnt[t] = 0;
-  if (t >= nq) return;
-  pl.tauq[t] = __float_as_int(kInf);
-  int fp = nprobe;
-  if (!pl.seed) {  // no seed pass: every usable probe goes to phase B
-    pl.first_probe[t] = nprobe;
-    return;
-  }
-  for (int p = 0; p < nprobe; p++)
-    if (usable_list(lists[t * nprobe + p], lo, hi, list_off)) {
-      fp = p;
-      break;
-    }
-  pl.first_probe[t] = fp;
-}
-
-__global__ __launch_bounds__(256) void k_bucket_count(const int64_t* __restrict__ lists, int64_t nq, int nprobe,
-                                                      const int64_t* __restrict__ list_off, int lo, int hi,
-                                                      ListPlan pl) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nq * nprobe) return;
-  const int64_t l = lists[i];
-  int s = -1;
-  if (usable_list(l, lo, hi, list_off) && (int)(i % nprobe) != pl.first_probe[i / nprobe])
-    s = atomicAdd(&pl.cnt[(int)(l - lo)], 1);
-  pl.slot[i] = s;
-}
-
-__global__ __launch_bounds__(PLAN_T) void k_bucket_plan(int lo, int hi, int G, const int64_t* __restrict__ list_off,
-                                                        ListPlan pl) {
-  __shared__ int32_t part[PLAN_T];
-  const int tid = threadIdx.x;
-  const int nloc = hi - lo;
-  const int chunk = (nloc + PLAN_T - 1) / PLAN_T;
-  const int j0 = min(nloc, tid * chunk), j1 = min(nloc, j0 + chunk);
-  int si = 0;
-  for (int j = j0; j < j1; j++) si += (pl.cnt[j] + G - 1) / G;
-  // exclusive prefix sum over the workgroup: wave scans (shuffles), then the
-  // 16 wave totals through LDS (two barriers instead of twenty)
-  const int lane = tid & 63, wave = tid >> 6;
-  int incl = si;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
-  }
-  if (lane == 63) part[wave] = incl;
-  __syncthreads();
-  int before = 0;
-  for (int w = 0; w < wave; w++) before += part[w];
-  int io = before + incl - si;
-  for (int j = j0; j < j1; j++) {
-    const int c = pl.cnt[j];
-    pl.cnt[j] = 0;  // invariant: counters are zero between batches (the coarse epilogue counts into them)
-    pl.ioff[j] = io;
-    const int nit = (c + G - 1) / G;
-    const int64_t beg = nit ? list_off[lo + j] : 0;
-    const int32_t sz = nit ? (int32_t)(list_off[lo + j + 1] - beg) : 0;
-    for (int t = 0; t < nit; t++) {
-      int32_t* r = pl.recs + (int64_t)(io + t) * 16;
-      r[0] = lo + j;
-      r[1] = min(G, c - t * G);
-      r[2] = sz;
-      r[3] = (int32_t)(uint32_t)(uint64_t)beg;
-      r[4] = (int32_t)(uint32_t)((uint64_t)beg >> 32);
-    }
-    io += nit;
-  }
-  if (tid == PLAN_T - 1) pl.n_items[0] = before + incl;
-  if (tid < 8) pl.n_items[1 + tid] = 0;  // per-XCD-group work counters of phase B
-}
-
-// scatter each phase-B pair id into its work item record
-__global__ __launch_bounds__(256) void k_bucket_scatter(const int64_t* __restrict__ lists,
-                                                        const float* __restrict__ dis0, int64_t nq, int nprobe, int lo,
-                                                        int G, ListPlan pl) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nq * nprobe) return;
-  const int s = pl.slot[i];
-  if (s < 0) return;
-  const int item = pl.ioff[(int)(lists[i] - lo)] + s / G;
-  int32_t* r = pl.recs + (int64_t)item * 16;
-  r[5 + s % G] = (int32_t)i;
-  r[9 + s % G] = __float_as_int(dis0 ? dis0[i] : 0.f);
-}
-
 template <int G>
-struct LutVec;
-template <>
-struct LutVec<1> {
-  using T = float;
-};
-template <>
-struct LutVec<2> {
-  using T = float2;
-};
-template <>
-struct LutVec<4> {
-  using T = float4;
+struct Item {
+  int l, cnt, n;
+  int64_t beg;
+  int pair[G];
+  float d0[G];
 };
 
-__device__ __forceinline__ float comp(float v, int) { return v; }
-__device__ __forceinline__ float comp(float2 v, int g) { return g == 0 ? v.x : v.y; }
-__device__ __forceinline__ float comp(float4 v, int g) { return g == 0 ? v.x : g == 1 ? v.y : g == 2 ? v.z : v.w; }
-__device__ __forceinline__ void setc(float& o, int, float x) { o = x; }
-__device__ __forceinline__ void setc(float2& o, int g, float x) {
-  if (g == 0) o.x = x; else o.y = x;
-}
-__device__ __forceinline__ void setc(float4& o, int g, float x) {
-  if (g == 0) o.x = x; else if (g == 1) o.y = x; else if (g == 2) o.z = x; else o.w = x;
-}
-
-// Phase B.  Persistent workgroups; each walks the work items of its XCD group
-// (blocks b and b+8 share an XCD, so the consecutive items of one list -- same
-// T1 row, same codes -- stay on one L2).  A work item is (list l, up to G
-// queries); the G LUTs are interleaved per entry ([m][j][g]) so one
-// ds_read_b{32,64,128} returns the G lookups of a code and the bank conflicts of
-// the random 8-bit gathers are paid once per G lookups.
-// Each wave issues all its code loads of a batch (up to J codes per lane) at
-// once, with clamped addresses so the load sequence is branch-free and the
-// compiler's vmcnt waits stay counted.  Candidates (dis <= min(own k-th,
-// tau_q)) go to a per-wave LDS queue that one compact loop drains into the
-// wave's per-query top-k, ranked by (distance, code position): device lists are
-// label-sorted, so this equals (distance, label) inside a list.  tau_q is shared
-// across workgroups through global atomicMin (any k real candidates bound the
-// final k-th; a stale read is only a looser bound).
-#ifndef SCAN_VAR
-#define SCAN_VAR 0  // experiment switch: gather order in k_scan_lists
-#endif
-#ifndef SCAN_J16
-#define SCAN_J16 4
-#endif
+// Persistent workgroups walk the work items: a workgroup starts in its XCD
+// group's chunk (blocks b and b + 8 share an XCD, so the consecutive items of
+// one list -- same T1 row, same codes -- stay on one L2), kind-0 items first,
+// then helps the other groups.  A work item is (list l, up to G pairs): the G
+// LUTs are interleaved per entry ([m][j][g]) so one ds_read_b{32,64,128}
+// returns the G lookups of a code and the bank conflicts of the random 8-bit
+// gathers are paid once per G lookups.  PF: the next item's record and T1/T3
+// rows are loaded into registers while the current item is scanned, so the
+// LUT build after the barrier never waits on memory.
+// Candidates (key <= min(own k-th, tau_q)) go to a per-wave LDS queue that one
+// compact loop drains into the wave's per-query top-k, ranked by (key, code
+// position): device lists are label-sorted, so this equals (key, label) inside
+// a list.  tau_q is shared across workgroups through global atomicMin (any k
+// real candidates bound the final k-th; a stale read is only a looser bound).
 constexpr int QCAP = 256;  // per-wave candidate queue entries
 
-template <int M, int G, int R, int J>
-__global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
+template <int M, int G, int R, int J, bool PF>
+__global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) {
   using V = typename LutVec<G>::T;
   constexpr int LUTN = M * 256;
   constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table
-  constexpr int KP = R * 64;
-  constexpr int LUT_BYTES = LUTN * (int)sizeof(V);
-  constexpr int MERGE_BYTES = 4 * KP * 12;
-  constexpr int SMEM = LUT_BYTES > MERGE_BYTES ? LUT_BYTES : MERGE_BYTES;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) V lut[LUTN];
   __shared__ float qd[4][QCAP];
   __shared__ int32_t qi[4][QCAP];  // (code position << 2) | g
-  V* lut = reinterpret_cast<V*>(smem);
+  __shared__ int s_next;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int k = a.k;
-  const int n_items = pl.n_items[0];
-  // a.debug & 8: one global work counter (A/B against per-XCD-group counters)
-  const bool global_q = (a.debug & 8) != 0;
-  const int per = global_q ? n_items : (n_items + 7) >> 3;
-  const int grp = global_q ? 0 : (blockIdx.x & 7);
-  const int c0 = grp * per;
-  const int c1 = min(n_items, c0 + per);
+  const int ip = a.ip;
+  const int nloc = a.list_hi - a.list_lo;
+  if (blockIdx.x == 0)  // the counts were consumed by k_plan_items: zero them for the next batch
+    for (int i = tid; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
+  const int n_items = pl.hdr[0], N0 = pl.hdr[1], N1 = n_items - N0;
+  const int per0 = (N0 + 7) >> 3, per1 = (N1 + 7) >> 3;
+  const int grp = blockIdx.x & 7;
+  int ngv = 0;  // groups exhausted so far (thread 0)
+  auto fetch = [&]() -> int {
+    while (ngv < 8) {
+      const int g = (grp + ngv) & 7;
+      const int a0 = g * per0, n0g = max(0, min(N0, a0 + per0) - a0);
+      const int a1 = g * per1, n1g = max(0, min(N1, a1 + per1) - a1);
+      const int t = atomicAdd(pl.hdr + 2 + g, 1);
+      if (t < n0g) return a0 + t;
+      if (t < n0g + n1g) return N0 + a1 + (t - n0g);
+      ngv++;
+    }
+    return -1;
+  };
   const uint64_t lanemask_lt = (1ull << lane) - 1;
 
-  int it_no = 0;
-  auto stamp = [&](int slot, uint64_t v) {
-    if (a.stamps && tid == 0 && it_no < kStampItems)
-      a.stamps[((int64_t)blockIdx.x * kStampItems + it_no) * kStampSlots + slot] = v;
-  };
-  // dynamic work fetching inside the XCD group (items vary from 1 to ~3k codes)
-  __shared__ int s_next;
-  int* ctr = pl.n_items + 1 + grp;
-  if (tid == 0) s_next = c0 + atomicAdd(ctr, 1);
-  __syncthreads();
-  for (int idx = s_next; idx < c1; idx = s_next, it_no++) {
-    __syncthreads();  // everyone has read s_next
-    if (tid == 0) s_next = c0 + atomicAdd(ctr, 1);  // consumed after this item
-    stamp(0, __builtin_amdgcn_s_memtime());
-    // one self-contained record: no dependent metadata loads
-    const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)idx * 16);
+  Item<G> it;
+  float4 t1v[PF ? NV : 1];
+  float4 t3v[G][PF ? NV : 1];
+  auto load_item = [&](int idx) {
+    const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)__builtin_amdgcn_readfirstlane(idx) * 16);
     const int4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
-    const int64_t l = r0.x;
-    const int cnt = r0.y;
-    const int n = r0.z;
-    const int64_t beg = (int64_t)(((uint64_t)(uint32_t)r1.x << 32) | (uint32_t)r0.w);
-    int pair[G];
-    int64_t qix[G];
-    float d0[G], bound[G];
+    it.l = r0.x;
+    it.cnt = r0.y;
+    it.n = r0.z;
+    it.beg = (int64_t)(((uint64_t)(uint32_t)r1.x << 32) | (uint32_t)r0.w);
+    const int pr[4] = {r1.y, r1.z, r1.w, r2.x};
+    const int db[4] = {r2.y, r2.z, r2.w, r3.x};
 #pragma unroll
     for (int g = 0; g < G; g++) {
-      const int pr = g == 0 ? r1.y : g == 1 ? r1.z : g == 2 ? r1.w : r2.x;
-      const int db = g == 0 ? r2.y : g == 1 ? r2.z : g == 2 ? r2.w : r3.x;
-      pair[g] = g < cnt ? pr : 0;
-      qix[g] = pair[g] / a.nprobe;
-      d0[g] = __int_as_float(db);
+      it.pair[g] = pr[g];
+      it.d0[g] = __int_as_float(db[g]);
     }
-    // every load of the item is issued before anything waits: T1/T3 rows,
-    // the query bounds and this wave's first batch of codes
-    float4 t1v[NV];
-    float4 t3v[G][NV];
-    {
-      const float4* T1l = reinterpret_cast<const float4*>(a.T1 + l * LUTN);
+  };
+  auto load_tables = [&](bool need_t1) {  // PF only
+    if constexpr (PF) {
+      if (need_t1 && !ip) {
+        const float4* T1l = reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
 #pragma unroll
-      for (int e = 0; e < NV; e++) t1v[e] = T1l[e * 256 + tid];
+        for (int e = 0; e < NV; e++) t1v[e] = T1l[e * 256 + tid];
+      }
 #pragma unroll
       for (int g = 0; g < G; g++) {
-        const float4* T3q = reinterpret_cast<const float4*>(a.T3 + qix[g] * LUTN);
+        if (g < it.cnt) {
+          const float4* T3q = reinterpret_cast<const float4*>(a.T3 + (int64_t)(it.pair[g] / a.nprobe) * LUTN);
 #pragma unroll
-        for (int e = 0; e < NV; e++) t3v[g][e] = T3q[e * 256 + tid];
+          for (int e = 0; e < NV; e++) t3v[g][e] = T3q[e * 256 + tid];
+        }
       }
     }
+  };
+
+  if (tid == 0) s_next = fetch();
+  __syncthreads();
+  int cur = s_next;
+  if (cur >= 0) {
+    load_item(cur);
+    if constexpr (PF) load_tables(true);
+  }
+  while (cur >= 0) {
+    __syncthreads();  // (A) every wave is done with the LUT of the previous item, and has read s_next
+    if (tid == 0) s_next = fetch();
+    // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
+    if constexpr (PF) {  // from the rows prefetched into registers
 #pragma unroll
-    for (int g = 0; g < G; g++) bound[g] = g < cnt ? __int_as_float(pl.tauq[qix[g]]) : -kInf;
-    const uint8_t* lc = a.codes + beg * M;
+      for (int e = 0; e < NV; e++) {
+        const int v = e * 256 + tid;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          V o;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const float t3 = comp(t3v[g][e], c);
+            const float lv = ip ? -t3 : comp(t1v[e], c) + (-2.0f * t3);
+            setc(o, g, g < it.cnt ? lv : 0.f);
+          }
+          lut[4 * v + c] = o;
+        }
+      }
+    } else {  // straight from memory, one float4 of each row at a time
+      const float4* T1l = reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
+      const float4* T3q[G];
+#pragma unroll
+      for (int g = 0; g < G; g++)
+        T3q[g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)((g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe) * LUTN);
+#pragma unroll 4
+      for (int e = 0; e < NV; e++) {
+        const int v = e * 256 + tid;
+        const float4 t1 = ip ? make_float4(0.f, 0.f, 0.f, 0.f) : T1l[v];
+        float4 t3[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) t3[g] = T3q[g][v];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          V o;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const float x3 = comp(t3[g], c);
+            const float lv = ip ? -x3 : comp(t1, c) + (-2.0f * x3);
+            setc(o, g, g < it.cnt ? lv : 0.f);
+          }
+          lut[4 * v + c] = o;
+        }
+      }
+    }
+    __syncthreads();  // (B) the LUT and s_next are visible
+    const Item<G> ci = it;
+    const int nxt = s_next;
+    const int n = ci.n;
+    const uint8_t* lc = a.codes + ci.beg * M;
     CodeWords<M> cw[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
       const int i = j * 256 + wave * 64 + lane;
-      cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
+      cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
     }
-    __syncthreads();  // the previous item is done with the LDS
-#pragma unroll
-    for (int e = 0; e < NV; e++) {
-      const int v = e * 256 + tid;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        V o;
-#pragma unroll
-        for (int g = 0; g < G; g++) setc(o, g, comp(t1v[e], c) + (-2.0f * comp(t3v[g][e], c)));
-        lut[4 * v + c] = o;
+    if constexpr (PF) {
+      if (nxt >= 0) {
+        load_item(nxt);
+        load_tables(it.l != ci.l);  // a run of items of one list keeps its T1 row
       }
     }
-    __syncthreads();
-    stamp(1, __builtin_amdgcn_s_memtime());
+    int64_t qix[G];
+    float bound[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      qix[g] = (g < ci.cnt ? ci.pair[g] : 0) / a.nprobe;
+      bound[g] = g < ci.cnt ? ord2f(pl.tauq[qix[g]]) : -kInf;
+    }
 
     WaveTopK<R> tk[G];
 #pragma unroll
@@ -1332,9 +1258,9 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
       for (int b0 = 0; b0 < qn; b0 += 64) {
         const int e = b0 + lane;
         const float cd = e < qn ? qd[wave][e] : kInf;
-        const int ci = e < qn ? qi[wave][e] : 0;
-        const int64_t pos = ci >> 2;
-        const int cg = ci & 3;
+        const int cidx = e < qn ? qi[wave][e] : 0;
+        const int64_t pos = cidx >> 2;
+        const int cg = cidx & 3;
 #pragma unroll
         for (int g = 0; g < G; g++) {
           const bool p = e < qn && cg == g && lexless(cd, pos, tk[g].td, tk[g].ti);
@@ -1355,7 +1281,7 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
       qn = 0;
 #pragma unroll
       for (int g = 0; g < G; g++) {
-        if (g < cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], __float_as_int(tk[g].td));
+        if (g < ci.cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td));
       }
     };
     auto push = [&](bool pass, uint64_t mask, float dv, int i, int g) {
@@ -1372,41 +1298,17 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
 #pragma unroll
         for (int j = 0; j < J; j++) {
           const int i = base + j * 256 + wave * 64 + lane;
-          cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
+          cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
         }
       }
-      // all J x G distances first, m-outer: J independent LDS gathers in flight
-      // per step and no control flow between them (per-chain order is the
+      // all J x G keys first, m-outer: J independent LDS gathers in flight per
+      // step and no control flow between them (per-chain order is the
       // sequential m order of the oracle)
       float dis[J][G];
 #pragma unroll
       for (int j = 0; j < J; j++)
 #pragma unroll
-        for (int g = 0; g < G; g++) dis[j][g] = d0[g];
-#if SCAN_VAR == 1
-#pragma unroll
-      for (int j = 0; j < J; j++) {
-#pragma unroll
-        for (int m = 0; m < M; m++) {
-          const V v = lut[m * 256 + cw[j].byte(m)];
-#pragma unroll
-          for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
-        }
-      }
-#elif SCAN_VAR == 2
-#pragma unroll
-      for (int j0 = 0; j0 < J; j0 += 2) {
-#pragma unroll
-        for (int m = 0; m < M; m++) {
-#pragma unroll
-          for (int j = j0; j < j0 + 2; j++) {
-            const V v = lut[m * 256 + cw[j].byte(m)];
-#pragma unroll
-            for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
-          }
-        }
-      }
-#else
+        for (int g = 0; g < G; g++) dis[j][g] = ci.d0[g];
 #pragma unroll
       for (int m = 0; m < M; m++) {
 #pragma unroll
@@ -1415,14 +1317,6 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
 #pragma unroll
           for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
         }
-      }
-#endif
-      if (a.debug & 1) {
-#pragma unroll
-        for (int j = 0; j < J; j++)
-#pragma unroll
-          for (int g = 0; g < G; g++) asm volatile("" ::"v"(dis[j][g]));
-        continue;
       }
       // push the J chunks' candidates while they fit; otherwise drain (which
       // also tightens the bounds) and resume.  One drain site keeps code size down.
@@ -1457,31 +1351,30 @@ __global__ __launch_bounds__(256) void k_scan_lists(ScanArgs a, ListPlan pl) {
     }
     if (qn > 0) drain();
 
-    stamp(2, __builtin_amdgcn_s_memtime());
-    stamp(4, (uint64_t)n);
-    stamp(5, (uint64_t)cnt);
-    // each wave writes its own sorted partial list per query (no in-workgroup merge)
+    // each wave writes its own sorted partial list per pair (merged by k_merge_probes)
 #pragma unroll
     for (int g = 0; g < G; g++) {
-      if (g >= cnt) continue;
-      const int64_t o = ((int64_t)pair[g] * 4 + wave) * k;
+      if (g >= ci.cnt) continue;
+      const int64_t o = ((int64_t)ci.pair[g] * 4 + wave) * k;
 #pragma unroll
       for (int r = 0; r < R; r++) {
         const int ix = r * 64 + lane;
         if (ix < k) {
           const bool empty = tk[g].id[r] == kSentinelId;
           pl.partD[o + ix] = empty ? FLT_MAX : tk[g].d[r];
-          pl.partI[o + ix] = empty ? -1 : beg + tk[g].id[r];  // global code position
+          pl.partI[o + ix] = empty ? -1 : ci.beg + tk[g].id[r];  // global code position
         }
       }
     }
-    stamp(3, __builtin_amdgcn_s_memtime());
-    __syncthreads();  // s_next is visible
+    if constexpr (!PF) {
+      if (nxt >= 0) load_item(nxt);
+    }
+    cur = nxt;
   }
 }
 
 // Per query (one wave): merge the per-wave partial lists of every scanned
-// probe ([probe][4 waves][k], sorted by (distance, position)).  All entries are
+// probe ([probe][4 waves][k], sorted by (key, position)).  All entries are
 // fetched in batches of 64 lanes x B loads (one round trip per batch); labels
 // are looked up only for entries that can still enter the top-k.
 template <int R>
@@ -1492,9 +1385,11 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   if (q >= a.nq) return;
   const int k = a.k;
   const int np = a.nprobe;
+  const float pad = a.ip ? -FLT_MAX : FLT_MAX;
+  const float sgn = a.ip ? -1.f : 1.f;  // key -> reported value
   if (R == 1 && k <= 16 && np * 4 <= 64) {
     // fast path: lane j owns partial list j = (probe j/4, wave j%4), already
-    // sorted by (distance, label); one 64-way merge
+    // sorted by (key, label); one 64-way merge
     float d[16];
     int64_t id[16];
     const int p = min(lane >> 2, np - 1);
@@ -1525,7 +1420,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     wave_kway<16>(d, id, k, lane, od, oi);
     if (lane < k) {
       const bool empty = oi == kSentinelId;
-      a.outD[q * k + lane] = empty ? FLT_MAX : od;
+      a.outD[q * k + lane] = empty ? pad : sgn * od;
       a.outI[q * k + lane] = empty ? -1 : oi;
     }
     return;
@@ -1547,7 +1442,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       if (e < total) {
         const int p = e / per_probe;
         const int64_t l = a.probe_list[q * np + p];
-        const bool scanned = p < np && l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
+        const bool scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
         if (scanned) {
           d[b] = pd[e];
           pos[b] = pi[e];
@@ -1576,7 +1471,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     const int idx = r * 64 + lane;
     if (idx < k) {
       const bool empty = tk.id[r] == kSentinelId;
-      a.outD[q * k + idx] = empty ? FLT_MAX : tk.d[r];
+      a.outD[q * k + idx] = empty ? pad : sgn * tk.d[r];
       a.outI[q * k + idx] = empty ? -1 : tk.id[r];
     }
   }
@@ -1585,9 +1480,10 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
 // ------------------------------------------------------------ shard merge
 __global__ __launch_bounds__(256) void k_merge_topk(int S, int64_t n, int k, const float* __restrict__ Din,
                                                     const int64_t* __restrict__ Iin, float* __restrict__ Dout,
-                                                    int64_t* __restrict__ Iout) {
+                                                    int64_t* __restrict__ Iout, int ip) {
   const int64_t q = blockIdx.x;
-  auto key_d = [&](int s, int j) { return Din[((int64_t)s * n + q) * k + j]; };
+  const float sgn = ip ? -1.f : 1.f;
+  auto key_d = [&](int s, int j) { return sgn * Din[((int64_t)s * n + q) * k + j]; };
   auto key_i = [&](int s, int j) {
     const int64_t v = Iin[((int64_t)s * n + q) * k + j];
     return v < 0 ? kSentinelId : v;
@@ -1615,7 +1511,7 @@ __global__ __launch_bounds__(256) void k_merge_topk(int S, int64_t n, int k, con
     }
     if (rank < k) {
       const bool empty = vi == kSentinelId;
-      Dout[q * k + rank] = empty ? FLT_MAX : vd;
+      Dout[q * k + rank] = empty ? (ip ? -FLT_MAX : FLT_MAX) : sgn * vd;
       Iout[q * k + rank] = empty ? -1 : vi;
     }
   }
@@ -1625,6 +1521,8 @@ inline unsigned nblocks(int64_t n, int per) { return (unsigned)((n + per - 1) / 
 
 inline int rows_for(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : k <= 256 ? 4 : k <= 512 ? 8 : 16; }
 
+size_t coarse_smem(int nlist, int d) { return sizeof(float) * (CQ * (size_t)d + CQ + (size_t)CQ * nlist); }
+
 }  // namespace
 
 void launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t s) {
@@ -1633,63 +1531,72 @@ void launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t 
 }
 
 void launch_l2_dist(const float* x, const float* xn, int64_t nx, const float* c, const float* cn, int nc, int d,
-                    float* out, hipStream_t s) {
+                    float* out, hipStream_t s, bool ip) {
   if (nx <= 0 || nc <= 0) return;
   dim3 grid(nblocks(nc, DT_B), nblocks(nx, DT_B));
-  hipLaunchKernelGGL(k_l2_dist, grid, dim3(256), 0, s, x, xn, nx, c, cn, nc, d, out);
+  hipLaunchKernelGGL(k_l2_dist, grid, dim3(256), 0, s, x, xn, nx, c, cn, nc, d, out, ip ? 1 : 0);
 }
 
 void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, float* ov, int64_t* oc,
-                        hipStream_t s) {
+                        hipStream_t s, bool neg) {
   if (nrows <= 0) return;
   const dim3 grid(nblocks(nrows, 4));
+  const int ng = neg ? 1 : 0;
   switch (rows_for(n)) {
-    case 1: hipLaunchKernelGGL(k_select_rows<1>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc); break;
-    case 2: hipLaunchKernelGGL(k_select_rows<2>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc); break;
-    case 4: hipLaunchKernelGGL(k_select_rows<4>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc); break;
-    case 8: hipLaunchKernelGGL(k_select_rows<8>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc); break;
-    default: hipLaunchKernelGGL(k_select_rows<16>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc); break;
+    case 1: hipLaunchKernelGGL(k_select_rows<1>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc, ng); break;
+    case 2: hipLaunchKernelGGL(k_select_rows<2>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc, ng); break;
+    case 4: hipLaunchKernelGGL(k_select_rows<4>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc, ng); break;
+    case 8: hipLaunchKernelGGL(k_select_rows<8>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc, ng); break;
+    default: hipLaunchKernelGGL(k_select_rows<16>, grid, dim3(256), 0, s, dist, nrows, ncols, n, ov, oc, ng); break;
   }
 }
 
-void set_coarse_debug(int v) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_coarse_debug), &v, sizeof(int)); }
+bool coarse_fused_ok(int nlist, int nprobe, int d) {
+  (void)nprobe;
+  return nlist <= kCoarseFusedMax && coarse_smem(nlist, d) <= 160 * 1024;
+}
 
 void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, ListPlan* plan,
-                         const int64_t* list_off, int lo, int hi, float* T3out, const float* cb, int M) {
+                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, bool ip, const ListPlan* plan,
+                         const int64_t* list_off, int lo, int hi, const float* cent, float* T3out, const float* cb,
+                         int M) {
   if (nq <= 0) return;
   CoarsePlan cp;
   if (plan && nprobe <= 64) {
+    cp.pl = *plan;
+    cp.on = 1;
     cp.list_off = list_off;
     cp.lo = lo;
     cp.hi = hi;
-    cp.pl = *plan;
-    plan->counted = 1;
+    cp.cent = cent;
   }
   if (T3out && M > 0 && d % M == 0) {
     cp.T3out = T3out;
     cp.cb = cb;
     cp.M = M;
-    if (plan) plan->t3done = 1;
   }
-  const size_t smem = sizeof(float) * (CQ * d + CQ + (size_t)CQ * nlist);
+  const size_t smem = coarse_smem(nlist, d);
   const dim3 grid(nblocks(nq, CQ));
-  static bool attr_set = false;
-  if (!attr_set) {  // dynamic LDS above 64 KiB must be opted into
+  // dynamic LDS above 64 KiB must be opted into, per device (function attributes are per device)
+  static uint64_t attr_done = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 64 && !(attr_done & (1ull << dev))) {
     const int lim = 160 * 1024;
     (void)hipFuncSetAttribute((const void*)k_coarse_fused<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void*)k_coarse_fused<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void*)k_coarse_fused<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void*)k_coarse_fused<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
     (void)hipFuncSetAttribute((const void*)k_coarse_fused<16>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    attr_set = true;
+    attr_done |= 1ull << dev;
   }
+  const int ipi = ip ? 1 : 0;
   switch (rows_for(nprobe)) {
-    case 1: hipLaunchKernelGGL(k_coarse_fused<1>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
-    case 2: hipLaunchKernelGGL(k_coarse_fused<2>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
-    case 4: hipLaunchKernelGGL(k_coarse_fused<4>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
-    case 8: hipLaunchKernelGGL(k_coarse_fused<8>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
-    default: hipLaunchKernelGGL(k_coarse_fused<16>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, cp); break;
+    case 1: hipLaunchKernelGGL(k_coarse_fused<1>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
+    case 2: hipLaunchKernelGGL(k_coarse_fused<2>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
+    case 4: hipLaunchKernelGGL(k_coarse_fused<4>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
+    case 8: hipLaunchKernelGGL(k_coarse_fused<8>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
+    default: hipLaunchKernelGGL(k_coarse_fused<16>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
   }
 }
 
@@ -1722,60 +1629,33 @@ void launch_pq_encode(const float* x, int64_t n, int d, const float* cent, const
                      codes);
 }
 
+void launch_plan_count(const int64_t* lists, const float* Dq, const float* x, const float* cent, int64_t nq, int d,
+                       int nprobe, const int64_t* list_off, int lo, int hi, bool ip, bool dedup, int k,
+                       const ListPlan& pl, hipStream_t s) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(k_plan_count, dim3(nblocks(nq, 4)), dim3(256), 0, s, lists, Dq, x, cent, nq, d, nprobe,
+                     list_off, lo, hi, ip ? 1 : 0, dedup ? 1 : 0, k, pl);
+}
+
+void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int hi, int G, hipStream_t s) {
+  const int nloc = hi - lo;
+  hipLaunchKernelGGL(k_plan_items, dim3(std::max(1u, nblocks(nloc, PLAN_T))), dim3(PLAN_T), 0, s, pl, list_off, lo,
+                     nloc, G);
+}
+
 bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 || M == 64; }
-
-template <int M>
-static void launch_scan_M(const ScanArgs& a, hipStream_t s) {
-  const dim3 grid((unsigned)a.nq);
-  switch (rows_for(a.k)) {
-    case 1: hipLaunchKernelGGL((k_scan_topk<M, 1, false>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_scan_topk<M, 2, false>), grid, dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_scan_topk<M, 4, false>), grid, dim3(256), 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_scan_topk<M, 8, false>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((k_scan_topk<M, 16, false>), grid, dim3(256), 0, s, a); break;
-  }
-}
-
-void launch_scan_topk(const ScanArgs& a, hipStream_t s) {
-  if (a.nq <= 0) return;
-  switch (a.M) {
-    case 8: launch_scan_M<8>(a, s); break;
-    case 16: launch_scan_M<16>(a, s); break;
-    case 32: launch_scan_M<32>(a, s); break;
-    case 48: launch_scan_M<48>(a, s); break;
-    case 64: launch_scan_M<64>(a, s); break;
-    default: break;
-  }
-}
 
 int list_scan_group(int M, int k) {
   const int R = rows_for(k);
   int G = 4;
-  while (G > 1 && (M * 1024 * G > 65536 || G * R > 16)) G >>= 1;
+  while (G > 1 && (M * 1024 * G > 65536 || G * R > 8)) G >>= 1;
   return G;
 }
 
-int list_scan_cap(int64_t nq, int nprobe, int nloc, int G) {
-  const int64_t p1 = nq * (nprobe > 1 ? nprobe - 1 : 0);
-  const int64_t v = std::min<int64_t>(nloc, p1) + (p1 + G - 1) / G + 8;
-  return (int)(((v + 7) / 8) * 8);
-}
-
-template <int M, int R>
-static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
-  constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 16) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 16) ? 2 : 1;
-  constexpr int J = M <= 8 ? 8 : M <= 16 ? SCAN_J16 : 2;  // codes per lane per batch (register budget)
-  ScanArgs seed = a;
-  seed.first_probe = pl.first_probe;
-  seed.partD = pl.partD;
-  seed.partI = pl.partI;
-  seed.tauq = pl.tauq;
-  seed.stamps = a.stamps ? a.stamps + (size_t)scan_lists_grid() * kStampItems * kStampSlots : nullptr;
-  if (pl.seed) hipLaunchKernelGGL((k_scan_topk<M, R, true>), dim3((unsigned)a.nq), dim3(256), 0, s, seed);
-  if (ev) (void)hipEventRecord(ev[0], s);
-  hipLaunchKernelGGL((k_scan_lists<M, G, R, J>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
-  if (ev) (void)hipEventRecord(ev[1], s);
-  hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
+int list_scan_max_items(int64_t npairs, int nloc, int G) {
+  // sum over (list, kind) buckets of ceil(c / G) <= npairs / G + (non-empty buckets)
+  const int64_t v = (npairs + G - 1) / G + std::min<int64_t>(2 * (int64_t)nloc, npairs) + 8;
+  return (int)v;
 }
 
 int scan_lists_grid() {
@@ -1786,6 +1666,18 @@ int scan_lists_grid() {
     grid = std::max(8, (2 * cus + 7) / 8 * 8);
   }
   return grid;
+}
+
+template <int M, int R>
+static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
+  constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 8) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 8) ? 2 : 1;
+  constexpr int J = M <= 8 ? 8 : M <= 16 ? 4 : 2;  // codes per lane per batch (register budget)
+  constexpr int NV = M / 4;
+  constexpr bool PF = NV * (G + 1) <= 24 && R <= 2;  // register prefetch of the next item's tables
+  if (ev) (void)hipEventRecord(ev[0], s);
+  hipLaunchKernelGGL((k_scan_lists<M, G, R, J, PF>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+  if (ev) (void)hipEventRecord(ev[1], s);
+  hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
 
 template <int M>
@@ -1801,40 +1693,20 @@ static void launch_lists_M(const ScanArgs& a, const ListPlan& pl, hipStream_t s,
 
 void launch_scan_lists(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev_lists) {
   if (a.nq <= 0) return;
-  const int G = list_scan_group(a.M, a.k);
-  const int64_t npairs = a.nq * a.nprobe;
-  const int nloc = a.list_hi - a.list_lo;
-  if (!pl.counted) {  // else done by the coarse epilogue (launch_coarse_fused with a plan)
-    hipLaunchKernelGGL(k_first_probe, dim3(nblocks(std::max<int64_t>(a.nq, (int64_t)nloc), 256)), dim3(256), 0, s,
-                       a.probe_list, a.nq, a.nprobe, a.list_off, a.list_lo, a.list_hi, pl);
-    hipLaunchKernelGGL(k_bucket_count, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.nq, a.nprobe,
-                       a.list_off, a.list_lo, a.list_hi, pl);
-  }
-  hipLaunchKernelGGL(k_bucket_plan, dim3(1), dim3(PLAN_T), 0, s, a.list_lo, a.list_hi, G, a.list_off, pl);
-  ScanArgs b = a;
-  if (pl.seed) {  // the seed launch scatters the pairs into the item records
-    b.scat_slot = pl.slot;
-    b.scat_ioff = pl.ioff;
-    b.scat_recs = pl.recs;
-    b.scat_G = G;
-  } else {
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(nblocks(npairs, 256)), dim3(256), 0, s, a.probe_list, a.probe_dis0,
-                       a.nq, a.nprobe, a.list_lo, G, pl);
-  }
   switch (a.M) {
-    case 8: launch_lists_M<8>(b, pl, s, ev_lists); break;
-    case 16: launch_lists_M<16>(b, pl, s, ev_lists); break;
-    case 32: launch_lists_M<32>(b, pl, s, ev_lists); break;
-    case 48: launch_lists_M<48>(b, pl, s, ev_lists); break;
-    case 64: launch_lists_M<64>(b, pl, s, ev_lists); break;
+    case 8: launch_lists_M<8>(a, pl, s, ev_lists); break;
+    case 16: launch_lists_M<16>(a, pl, s, ev_lists); break;
+    case 32: launch_lists_M<32>(a, pl, s, ev_lists); break;
+    case 48: launch_lists_M<48>(a, pl, s, ev_lists); break;
+    case 64: launch_lists_M<64>(a, pl, s, ev_lists); break;
     default: break;
   }
 }
 
 void launch_merge_topk(int S, int64_t n, int k, const float* Din, const int64_t* Iin, float* Dout, int64_t* Iout,
-                       hipStream_t s) {
+                       hipStream_t s, bool ip) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_merge_topk, dim3((unsigned)n), dim3(256), 0, s, S, n, k, Din, Iin, Dout, Iout);
+  hipLaunchKernelGGL(k_merge_topk, dim3((unsigned)n), dim3(256), 0, s, S, n, k, Din, Iin, Dout, Iout, ip ? 1 : 0);
 }
 
 }  // namespace chivf

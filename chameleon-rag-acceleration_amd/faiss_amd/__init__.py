@@ -10,6 +10,7 @@ from .index import (  # noqa: F401
     MAX_K,
     METRIC_INNER_PRODUCT,
     METRIC_L2,
+    IndexFlatIP,
     IndexFlatL2,
     IndexIVFPQ,
     ParameterSpace,

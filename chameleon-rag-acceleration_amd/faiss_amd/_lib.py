@@ -47,7 +47,7 @@ SIGNATURES = {
                                                        ctypes.c_void_p, ctypes.c_void_p]),
     "ivfpq_coarse_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
-    "ivfpq_merge_topk_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+    "ivfpq_merge_topk_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p]),
     "ivfpq_set_timing": (ctypes.c_int, [c_handle, ctypes.c_int]),
@@ -64,7 +64,7 @@ SIGNATURES = {
     "ivfpq_save": (ctypes.c_int, [c_handle, ctypes.c_char_p]),
     "ivfpq_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(c_handle)]),
     "ivfpq_flat_search": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, c_f32p, ctypes.c_int64,
-                                         c_f32p, ctypes.c_int, c_f32p, c_i64p]),
+                                         c_f32p, ctypes.c_int, ctypes.c_int, c_f32p, c_i64p]),
 }
 
 

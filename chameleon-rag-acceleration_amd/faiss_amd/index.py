@@ -117,8 +117,18 @@ class IndexFlatL2:
         I = np.empty((n, k), np.int64)
         L = _lib.load()
         _lib.check(L.ivfpq_flat_search(self.device, self.d, self.ntotal, _ptr(self._xb, _lib.c_f32p), n,
-                                       _ptr(x, _lib.c_f32p), k, _ptr(D, _lib.c_f32p), _ptr(I, _lib.c_i64p)))
+                                       _ptr(x, _lib.c_f32p), k, self.metric_type, _ptr(D, _lib.c_f32p),
+                                       _ptr(I, _lib.c_i64p)))
         return D, I
+
+
+class IndexFlatIP(IndexFlatL2):
+    """Exact inner-product search (faiss.IndexFlatIP): the quantizer of an
+    inner-product IndexIVFPQ and beir's flat IP index
+    (beir/beir/retrieval/search/dense/faiss_search.py:14-131).  Results are the
+    k largest inner products, descending."""
+
+    metric_type = METRIC_INNER_PRODUCT
 
 
 class _ProductQuantizer:
@@ -186,7 +196,8 @@ class _InvertedLists:
 
 
 class IndexIVFPQ:
-    """faiss.IndexIVFPQ (L2, by_residual, precomputed tables) on one MI355X."""
+    """faiss.IndexIVFPQ (by_residual; METRIC_L2 with precomputed tables, or
+    METRIC_INNER_PRODUCT) on one MI355X."""
 
     by_residual = True
     use_precomputed_table = 1
@@ -199,7 +210,9 @@ class IndexIVFPQ:
         self.nbits = int(nbits)
         self.metric_type = metric
         self.device = _default_device() if device is None else int(device)
-        self.quantizer = quantizer if quantizer is not None else IndexFlatL2(d, self.device)
+        if quantizer is None:
+            quantizer = (IndexFlatIP if metric == METRIC_INNER_PRODUCT else IndexFlatL2)(d, self.device)
+        self.quantizer = quantizer
         self.parallel_mode = 0  # accepted for faiss_retriever.py:71; queries are always independent
         self.verbose = False
         self.niter_coarse = 25
@@ -262,7 +275,7 @@ class IndexIVFPQ:
         return t.reshape(-1)
 
     def _sync_quantizer(self):
-        if isinstance(self.quantizer, IndexFlatL2):
+        if isinstance(self.quantizer, IndexFlatL2):  # IndexFlatIP too
             self.quantizer.reset()
             self.quantizer.add(self.centroids())
 
@@ -379,63 +392,106 @@ class IndexIVFPQ:
         return {s: (ms[i], cnt[i]) for i, s in enumerate(self.STAGES)}
 
     # ------------------------------------------------- device (torch) entry points
-    def search_device(self, x, k, D=None, I=None, stream=None):
-        """Search with inputs resident in HBM.  ``x`` is a torch float32 CUDA
-        tensor [n, d]; returns torch (D, I) on the same device, launched on
-        ``stream`` (default: torch's current stream)."""
+    def _check_dev(self, t, name, dtype, shape):
+        """The C-ABI takes raw device pointers: anything but a contiguous tensor of
+        the exact dtype and shape on this index's device would be read or written
+        out of bounds, so it is rejected here (as the host path rejects bad arrays)."""
+        import torch
+
+        if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+            raise RuntimeError(f"{name} must be a CUDA tensor")
+        if t.device.index != self.device:
+            raise RuntimeError(f"{name} is on cuda:{t.device.index}, the index on cuda:{self.device}")
+        if t.dtype != dtype:
+            raise RuntimeError(f"{name} must be {dtype}, got {t.dtype}")
+        if tuple(t.shape) != tuple(shape):
+            raise RuntimeError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+        if not t.is_contiguous():
+            raise RuntimeError(f"{name} must be contiguous")
+        return t
+
+    def _dev_outputs(self, x, k, D, I):
         import torch
 
         n = x.shape[0]
-        self._check_k(k)
         if D is None:
             D = torch.empty((n, k), dtype=torch.float32, device=x.device)
         if I is None:
             I = torch.empty((n, k), dtype=torch.int64, device=x.device)
-        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
-        _lib.check(_lib.load().ivfpq_search_device(self._h, n, x.data_ptr(), int(k), D.data_ptr(), I.data_ptr(),
-                                                   ctypes.c_void_p(s)))
+        self._check_dev(D, "D", torch.float32, (n, k))
+        self._check_dev(I, "I", torch.int64, (n, k))
+        return D, I
+
+    def _stream(self, x, stream):
+        import torch
+
+        return stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+
+    def search_device(self, x, k, D=None, I=None, stream=None):
+        """Search with inputs resident in HBM.  ``x`` is a torch float32 CUDA
+        tensor [n, d] on the index's device; returns torch (D, I) there, launched
+        on ``stream`` (default: torch's current stream).  Searches of one index
+        may be issued on different streams without synchronizing (the library
+        orders them)."""
+        import torch
+
+        self._check_k(k)
+        self._check_dev(x, "x", torch.float32, (x.shape[0] if x.dim() == 2 else -1, self.d))
+        D, I = self._dev_outputs(x, k, D, I)
+        _lib.check(_lib.load().ivfpq_search_device(self._h, x.shape[0], x.data_ptr(), int(k), D.data_ptr(),
+                                                   I.data_ptr(), ctypes.c_void_p(self._stream(x, stream))))
         return D, I
 
     def search_preassigned_device(self, x, k, Iq, Dq=None, D=None, I=None, stream=None):
         import torch
 
-        n = x.shape[0]
         self._check_k(k)
-        if D is None:
-            D = torch.empty((n, k), dtype=torch.float32, device=x.device)
-        if I is None:
-            I = torch.empty((n, k), dtype=torch.int64, device=x.device)
-        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        n = x.shape[0] if x.dim() == 2 else -1
+        self._check_dev(x, "x", torch.float32, (n, self.d))
+        self._check_dev(Iq, "Iq", torch.int64, (n, self.nprobe))
+        if Dq is not None:
+            self._check_dev(Dq, "Dq", torch.float32, (n, self.nprobe))
+        D, I = self._dev_outputs(x, k, D, I)
         _lib.check(_lib.load().ivfpq_search_preassigned_device(
             self._h, n, x.data_ptr(), int(k), Iq.data_ptr(), Dq.data_ptr() if Dq is not None else None,
-            D.data_ptr(), I.data_ptr(), ctypes.c_void_p(s)))
+            D.data_ptr(), I.data_ptr(), ctypes.c_void_p(self._stream(x, stream))))
         return D, I
 
     def coarse_device(self, x, Iq=None, Dq=None, stream=None):
+        """The coarse quantizer alone: (Dq, Iq) [n, min(nprobe, nlist)] -- L2
+        distances ascending or inner products descending."""
         import torch
 
-        n = x.shape[0]
+        n = x.shape[0] if x.dim() == 2 else -1
+        self._check_dev(x, "x", torch.float32, (n, self.d))
         p = min(self.nprobe, self.nlist)
         if Iq is None:
             Iq = torch.empty((n, p), dtype=torch.int64, device=x.device)
         if Dq is None:
             Dq = torch.empty((n, p), dtype=torch.float32, device=x.device)
-        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        self._check_dev(Iq, "Iq", torch.int64, (n, p))
+        self._check_dev(Dq, "Dq", torch.float32, (n, p))
         _lib.check(_lib.load().ivfpq_coarse_device(self._h, n, x.data_ptr(), Iq.data_ptr(), Dq.data_ptr(),
-                                                   ctypes.c_void_p(s)))
+                                                   ctypes.c_void_p(self._stream(x, stream))))
         return Dq, Iq
 
 
-def merge_topk_device(Ds, Is, stream=None):
-    """Merge S sorted partial results (torch [S, n, k]) into [n, k] on the GPU."""
+def merge_topk_device(Ds, Is, metric=METRIC_L2, stream=None):
+    """Merge S sorted partial results (torch [S, n, k]) into [n, k] on the GPU:
+    ascending L2 distances, or descending inner products (metric)."""
     import torch
 
+    if Ds.dim() != 3 or Is.shape != Ds.shape or Ds.dtype != torch.float32 or Is.dtype != torch.int64:
+        raise RuntimeError("merge_topk_device: Ds float32 [S, n, k] and Is int64 of the same shape")
+    if not (Ds.is_cuda and Is.is_cuda and Ds.device == Is.device):
+        raise RuntimeError("merge_topk_device: inputs must be on one CUDA device")
+    Ds, Is = Ds.contiguous(), Is.contiguous()
     S, n, k = Ds.shape
     D = torch.empty((n, k), dtype=torch.float32, device=Ds.device)
     I = torch.empty((n, k), dtype=torch.int64, device=Ds.device)
     s = stream if stream is not None else torch.cuda.current_stream(Ds.device).cuda_stream
-    _lib.check(_lib.load().ivfpq_merge_topk_device(S, n, k, Ds.data_ptr(), Is.data_ptr(), D.data_ptr(),
-                                                   I.data_ptr(), ctypes.c_void_p(s)))
+    _lib.check(_lib.load().ivfpq_merge_topk_device(S, n, k, int(metric), Ds.data_ptr(), Is.data_ptr(),
+                                                   D.data_ptr(), I.data_ptr(), ctypes.c_void_p(s)))
     return D, I
 
 
@@ -455,7 +511,7 @@ def parse_factory(key):
 def index_factory(d, key, metric=METRIC_L2, device=None):
     """faiss.index_factory(d, "IVF1024,PQ16") (bench_polysemous_1bn.py:272)."""
     nlist, M, nbits = parse_factory(key)
-    return IndexIVFPQ(IndexFlatL2(d, device), d, nlist, M, nbits, metric, device)
+    return IndexIVFPQ(None, d, nlist, M, nbits, metric, device)
 
 
 class ParameterSpace:

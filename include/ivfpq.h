@@ -8,13 +8,18 @@
  * device pointers plus a hipStream_t passed as void*.
  *
  * Conventions (as faiss.IndexIVFPQ):
- *   x: float32 [n][d] row-major;  D: float32 [n][k] ascending L2;
- *   I: int64 [n][k] labels, -1 (with distance FLT_MAX) where fewer than k
- *   results exist.  Ties are ordered by (distance, label).
+ *   x: float32 [n][d] row-major;  D: float32 [n][k] ascending L2 distances
+ *   (METRIC_L2) or descending inner products (METRIC_INNER_PRODUCT);
+ *   I: int64 [n][k] labels, -1 (with distance FLT_MAX, or -FLT_MAX for inner
+ *   product: the Faiss heap's neutral element) where fewer than k results
+ *   exist.  Ties are ordered by label.
  * Errors: every int-returning function returns 0 on success and -1 on error;
  * ivfpq_last_error() gives the thread-local message (the Python layer raises
  * RuntimeError, as Faiss's SWIG wrapper does for FaissException).
  * Thread-safety: one mutex per handle; train/add/search serialize on it.
+ * Stream ordering: a handle's device searches may be issued on different
+ * streams without synchronizing; each one waits (hipStreamWaitEvent) for the
+ * previous search on the handle, whose workspaces it reuses.
  */
 #ifndef CHAMELEON_IVFPQ_H
 #define CHAMELEON_IVFPQ_H
@@ -27,7 +32,7 @@ extern "C" {
 
 typedef struct ivfpq_index ivfpq_index;
 
-#define IVFPQ_METRIC_INNER_PRODUCT 0 /* faiss.METRIC_INNER_PRODUCT (not yet served on GPU) */
+#define IVFPQ_METRIC_INNER_PRODUCT 0 /* faiss.METRIC_INNER_PRODUCT (beir faiss_search.py:170, 194) */
 #define IVFPQ_METRIC_L2 1            /* faiss.METRIC_L2 */
 
 /* Last error message of the calling thread ("" if none). */
@@ -88,8 +93,9 @@ int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, i
 int ivfpq_coarse_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, float* Dq, void* stream);
 
 /* Merge S sorted partial results [S][n][k] into [n][k] on the device (the IndexShards
- * merge, bench_gpu_1bn.py:605-616; host argsort merge, bench_multi_cpu_performance_OSDI.py:203-218). */
-int ivfpq_merge_topk_device(int S, int64_t n, int k, const float* Din, const int64_t* Iin, float* Dout,
+ * merge, bench_gpu_1bn.py:605-616; host argsort merge, bench_multi_cpu_performance_OSDI.py:203-218).
+ * metric: IVFPQ_METRIC_L2 (partials ascending) or IVFPQ_METRIC_INNER_PRODUCT (descending). */
+int ivfpq_merge_topk_device(int S, int64_t n, int k, int metric, const float* Din, const int64_t* Iin, float* Dout,
                             int64_t* Iout, void* stream);
 
 /* Per-stage device timing (the nsys stage split of MICRO_GPU_profiling/classify_stages.py:113-181,
@@ -121,10 +127,11 @@ int ivfpq_get_precomputed_table(ivfpq_index* h, float* out);
 int ivfpq_save(ivfpq_index* h, const char* path);
 int ivfpq_load(const char* path, int device, ivfpq_index** out);
 
-/* Brute-force exact L2 k-NN on the GPU (IndexFlatL2::search; the coarse-quantizer
- * service of ralm/index_scanner/index_scanner.py:61-77).  Host buffers. */
-int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n, const float* x, int k, float* D,
-                      int64_t* I);
+/* Brute-force exact k-NN on the GPU: IndexFlatL2::search (metric L2; the coarse-quantizer
+ * service of ralm/index_scanner/index_scanner.py:61-77) or IndexFlatIP::search (metric
+ * INNER_PRODUCT; beir faiss_search.py's flat IP indexes).  Host buffers. */
+int ivfpq_flat_search(int device, int d, int64_t nb, const float* xb, int64_t n, const float* x, int k, int metric,
+                      float* D, int64_t* I);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,15 @@
  *    retrieval_accelerator/entire_accelerator_final_SIFT_M16/src/ADC.hpp:86-90)
  *  - top-k: the k smallest (dis, label) pairs, lexicographic;
  *    missing results are (FLT_MAX, -1).
+ *  - METRIC_INNER_PRODUCT (beir's default, beir/beir/retrieval/search/dense/
+ *    faiss_search.py:170, 194), Faiss 1.7.1 by-residual IP semantics
+ *    (IVFPQScanner<METRIC_INNER_PRODUCT, CMin>, precompute_list_tables_IP):
+ *    coarse = IndexFlatIP (k-ordered fmaf chain, the nprobe LARGEST);
+ *    per query LUT = T3 (no precomputed table); per probe
+ *    dis0 = tree_ip(q, c_l) over d (the coarse similarity is not reused);
+ *    per code dis = dis0 + sum_m T3[m][code[m]] in order; the k LARGEST,
+ *    ties by label; missing results are (-FLT_MAX, -1) (CMin's neutral).
+ *    Parity unpinned: the reference's NumPy oracle and the FPGA are L2-only.
  *  - encode (add): coarse top-1, residual r = x - c, per sub-quantizer the
  *    first argmin of tree_L2(r_m, C_mj)   (ProductQuantizer::compute_code).
  *  - k-means: this build's own deterministic Lloyd k-means (Faiss training is
@@ -102,13 +111,20 @@ static inline int or_less(float da, int64_t ia, float db, int64_t ib) {
     return da < db || (da == db && ia < ib);
 }
 
-/* max-heap on (dis, label): root = worst kept element */
-static void or_heap_push(float *hd, int64_t *hi, int *sz, int k, float d, int64_t id) {
+/* "a ranks before b": L2 ascending distance, IP descending similarity; ties by label */
+static inline int or_before(int ip, float da, int64_t ia, float db, int64_t ib) {
+    if (ip) return da > db || (da == db && ia < ib);
+    return or_less(da, ia, db, ib);
+}
+
+/* bounded heap on (dis, label) whose root is the worst kept element:
+ * L2 a max-heap of distances (Faiss CMax), IP a min-heap of similarities (CMin) */
+static void or_heap_push(int ip, float *hd, int64_t *hi, int *sz, int k, float d, int64_t id) {
     if (*sz < k) {
         int i = (*sz)++;
         while (i > 0) {
             int p = (i - 1) / 2;
-            if (!or_less(hd[p], hi[p], d, id)) break;
+            if (!or_before(ip, hd[p], hi[p], d, id)) break;
             hd[i] = hd[p];
             hi[i] = hi[p];
             i = p;
@@ -117,14 +133,14 @@ static void or_heap_push(float *hd, int64_t *hi, int *sz, int k, float d, int64_
         hi[i] = id;
         return;
     }
-    if (!or_less(d, id, hd[0], hi[0])) return;
+    if (!or_before(ip, d, id, hd[0], hi[0])) return;
     int i = 0;
     for (;;) {
         int l = 2 * i + 1, r = l + 1, c = i;
         float cd = d;
         int64_t ci = id;
-        if (l < k && or_less(cd, ci, hd[l], hi[l])) { c = l; cd = hd[l]; ci = hi[l]; }
-        if (r < k && or_less(cd, ci, hd[r], hi[r])) { c = r; }
+        if (l < k && or_before(ip, cd, ci, hd[l], hi[l])) { c = l; cd = hd[l]; ci = hi[l]; }
+        if (r < k && or_before(ip, cd, ci, hd[r], hi[r])) { c = r; }
         if (c == i) break;
         hd[i] = hd[c];
         hi[i] = hi[c];
@@ -134,8 +150,8 @@ static void or_heap_push(float *hd, int64_t *hi, int *sz, int k, float d, int64_
     hi[i] = id;
 }
 
-static void or_heap_sort_out(float *hd, int64_t *hi, int sz, int k, float *D, int64_t *I) {
-    /* pop max repeatedly into the back */
+static void or_heap_sort_out(int ip, float *hd, int64_t *hi, int sz, int k, float *D, int64_t *I) {
+    /* pop the worst repeatedly into the back */
     for (int n = sz; n > 0; n--) {
         float md = hd[0];
         int64_t mi = hi[0];
@@ -146,8 +162,8 @@ static void or_heap_sort_out(float *hd, int64_t *hi, int sz, int k, float *D, in
             int l = 2 * i + 1, r = l + 1, c = i;
             float cd = ld;
             int64_t ci = li;
-            if (l < m && or_less(cd, ci, hd[l], hi[l])) { c = l; cd = hd[l]; ci = hi[l]; }
-            if (r < m && or_less(cd, ci, hd[r], hi[r])) { c = r; }
+            if (l < m && or_before(ip, cd, ci, hd[l], hi[l])) { c = l; cd = hd[l]; ci = hi[l]; }
+            if (r < m && or_before(ip, cd, ci, hd[r], hi[r])) { c = r; }
             if (c == i) break;
             hd[i] = hd[c];
             hi[i] = hi[c];
@@ -157,16 +173,18 @@ static void or_heap_sort_out(float *hd, int64_t *hi, int sz, int k, float *D, in
         D[n - 1] = md;
         I[n - 1] = mi;
     }
-    for (int j = sz; j < k; j++) { D[j] = FLT_MAX; I[j] = -1; }
+    for (int j = sz; j < k; j++) { D[j] = ip ? -FLT_MAX : FLT_MAX; I[j] = -1; }
 }
 
 /* ---------------- coarse quantizer (IndexFlatL2::search) ---------------- */
 
-/* For each query the `nprobe` smallest coarse distances, ascending by
- * (dis, list id).  Reference call site: bench_polysemous_1bn.py:430 →
- * IndexIVF::search → quantizer->search. */
-void or_coarse_search(const float *x, int64_t n, int d, const float *cent, const float *cnorm,
-                      int nlist, int nprobe, int64_t *lists, float *dis, int nthreads) {
+/* For each query the `nprobe` best coarse lists: L2 the smallest distances,
+ * ascending by (dis, list id); IP (metric 0) the largest inner products,
+ * descending, ties by list id.  Reference call site: bench_polysemous_1bn.py:430
+ * → IndexIVF::search → quantizer->search. */
+void or_coarse_search_metric(const float *x, int64_t n, int d, const float *cent, const float *cnorm,
+                             int nlist, int nprobe, int64_t *lists, float *dis, int nthreads, int metric) {
+    const int ip = metric == 0;
     if (nprobe > nlist) nprobe = nlist;
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
     {
@@ -178,14 +196,20 @@ void or_coarse_search(const float *x, int64_t n, int d, const float *cent, const
             float xn = or_tree(xq, xq, d, OR_NORM);
             int sz = 0;
             for (int c = 0; c < nlist; c++) {
-                float dd = or_coarse_dis(xq, xn, cent + (int64_t)c * d, cnorm[c], d);
-                or_heap_push(hd, hi, &sz, nprobe, dd, c);
+                const float *cc = cent + (int64_t)c * d;
+                float dd = ip ? or_fma_dot(xq, cc, d) : or_coarse_dis(xq, xn, cc, cnorm[c], d);
+                or_heap_push(ip, hd, hi, &sz, nprobe, dd, c);
             }
-            or_heap_sort_out(hd, hi, sz, nprobe, dis + q * nprobe, lists + q * nprobe);
+            or_heap_sort_out(ip, hd, hi, sz, nprobe, dis + q * nprobe, lists + q * nprobe);
         }
         free(hd);
         free(hi);
     }
+}
+
+void or_coarse_search(const float *x, int64_t n, int d, const float *cent, const float *cnorm,
+                      int nlist, int nprobe, int64_t *lists, float *dis, int nthreads) {
+    or_coarse_search_metric(x, n, d, cent, cnorm, nlist, nprobe, lists, dis, nthreads, 1);
 }
 
 /* ---------------- PQ tables ---------------- */
@@ -221,9 +245,39 @@ void or_precompute_T1(const float *cent, int nlist, int d, const float *codebook
 
 /* ---------------- encode (add path) ---------------- */
 
+/* coarse assignment of one vector: L2 the first nearest centroid, IP (metric 0)
+ * the first largest inner product (IndexFlatIP as the IVF quantizer) */
+static inline int or_assign(const float *xi, float xn, const float *cent, const float *cnorm, int nlist, int d,
+                            int ip) {
+    int best = 0;
+    float bd = 0;
+    for (int c = 0; c < nlist; c++) {
+        const float *cc = cent + (int64_t)c * d;
+        if (ip) {
+            float dd = or_fma_dot(xi, cc, d);
+            if (c == 0 || dd > bd) { bd = dd; best = c; }
+        } else {
+            float dd = or_coarse_dis(xi, xn, cc, cnorm[c], d);
+            if (c == 0 || dd < bd) { bd = dd; best = c; }
+        }
+    }
+    return best;
+}
+
+void or_encode_metric(const float *x, int64_t n, int d, const float *cent, const float *cnorm, int nlist,
+                      const float *codebook, int M, int ksub, int64_t *list_no, uint8_t *codes, int nthreads,
+                      int metric);
+
 void or_encode(const float *x, int64_t n, int d, const float *cent, const float *cnorm, int nlist,
                const float *codebook, int M, int ksub, int64_t *list_no, uint8_t *codes, int nthreads) {
+    or_encode_metric(x, n, d, cent, cnorm, nlist, codebook, M, ksub, list_no, codes, nthreads, 1);
+}
+
+void or_encode_metric(const float *x, int64_t n, int d, const float *cent, const float *cnorm, int nlist,
+                      const float *codebook, int M, int ksub, int64_t *list_no, uint8_t *codes, int nthreads,
+                      int metric) {
     int dsub = d / M;
+    const int ip = metric == 0;
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
     {
         float *r = (float *)malloc(sizeof(float) * d);
@@ -231,12 +285,7 @@ void or_encode(const float *x, int64_t n, int d, const float *cent, const float 
         for (int64_t i = 0; i < n; i++) {
             const float *xi = x + i * d;
             float xn = or_tree(xi, xi, d, OR_NORM);
-            int best = 0;
-            float bd = 0;
-            for (int c = 0; c < nlist; c++) {
-                float dd = or_coarse_dis(xi, xn, cent + (int64_t)c * d, cnorm[c], d);
-                if (c == 0 || dd < bd) { bd = dd; best = c; }
-            }
+            int best = or_assign(xi, xn, cent, cnorm, nlist, d, ip);
             list_no[i] = best;
             const float *cb = cent + (int64_t)best * d;
             for (int t = 0; t < d; t++) r[t] = xi[t] - cb[t];
@@ -256,15 +305,17 @@ void or_encode(const float *x, int64_t n, int d, const float *cent, const float 
 
 /* ---------------- search over inverted lists ---------------- */
 
-/* IndexIVF::search_preassigned + IVFPQScanner (precompute mode 2, L2).
+/* IndexIVF::search_preassigned + IVFPQScanner (precompute mode 2).
  * lists / dis0: [n][nprobe]; list id < 0 = skipped probe.
- * list_off: [nlist+1] offsets into codes (in codes) and ids. */
-void or_search_preassigned(const float *x, int64_t n, int d, const float *T1, const float *codebook,
-                           int M, int ksub, const int64_t *list_off, const uint8_t *codes,
-                           const int64_t *ids, int nprobe, const int64_t *lists, const float *dis0,
-                           int k, float *D, int64_t *I, int nthreads) {
-    int dsub = d / M;
-    (void)dsub;
+ * list_off: [nlist+1] offsets into codes (in codes) and ids.
+ * metric 1 (L2): LUT = T1[l] + (-2) T3, dis0 = the given coarse distance.
+ * metric 0 (IP): LUT = T3, dis0 = tree_ip(q, centroid l) over d (cent), the
+ * given dis0 is ignored (precompute_list_tables_IP). */
+void or_search_preassigned_metric(const float *x, int64_t n, int d, const float *T1, const float *codebook,
+                                  int M, int ksub, const int64_t *list_off, const uint8_t *codes,
+                                  const int64_t *ids, int nprobe, const int64_t *lists, const float *dis0,
+                                  int k, float *D, int64_t *I, int nthreads, int metric, const float *cent) {
+    const int ip = metric == 0;
 #pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
     {
         float *t3 = (float *)malloc(sizeof(float) * M * ksub);
@@ -273,29 +324,49 @@ void or_search_preassigned(const float *x, int64_t n, int d, const float *T1, co
         int64_t *hi = (int64_t *)malloc(sizeof(int64_t) * k);
 #pragma omp for schedule(dynamic, 1)
         for (int64_t q = 0; q < n; q++) {
-            or_ip_table(x + q * d, 1, d, codebook, M, ksub, t3);
+            const float *xq = x + q * d;
+            or_ip_table(xq, 1, d, codebook, M, ksub, t3);
             int sz = 0;
             for (int p = 0; p < nprobe; p++) {
                 int64_t l = lists[q * nprobe + p];
                 if (l < 0) continue;
-                float d0 = dis0 ? dis0[q * nprobe + p] : 0.0f;
-                const float *t1 = T1 + l * M * ksub;
-                for (int e = 0; e < M * ksub; e++) lut[e] = t1[e] + (-2.0f * t3[e]);
+                int dup = 0; /* a list repeated in the row is scanned once */
+                for (int j = 0; j < p && !dup; j++) dup = lists[q * nprobe + j] == l;
+                if (dup) continue;
+                float d0;
+                const float *tab;
+                if (ip) {
+                    d0 = or_tree(xq, cent + l * d, d, OR_IP);
+                    tab = t3;
+                } else {
+                    d0 = dis0 ? dis0[q * nprobe + p] : 0.0f;
+                    const float *t1 = T1 + l * M * ksub;
+                    for (int e = 0; e < M * ksub; e++) lut[e] = t1[e] + (-2.0f * t3[e]);
+                    tab = lut;
+                }
                 int64_t beg = list_off[l], end = list_off[l + 1];
                 for (int64_t i = beg; i < end; i++) {
                     const uint8_t *c = codes + i * M;
                     float dis = d0;
-                    for (int m = 0; m < M; m++) dis = dis + lut[m * ksub + c[m]];
-                    or_heap_push(hd, hi, &sz, k, dis, ids[i]);
+                    for (int m = 0; m < M; m++) dis = dis + tab[m * ksub + c[m]];
+                    or_heap_push(ip, hd, hi, &sz, k, dis, ids[i]);
                 }
             }
-            or_heap_sort_out(hd, hi, sz, k, D + q * k, I + q * k);
+            or_heap_sort_out(ip, hd, hi, sz, k, D + q * k, I + q * k);
         }
         free(t3);
         free(lut);
         free(hd);
         free(hi);
     }
+}
+
+void or_search_preassigned(const float *x, int64_t n, int d, const float *T1, const float *codebook,
+                           int M, int ksub, const int64_t *list_off, const uint8_t *codes,
+                           const int64_t *ids, int nprobe, const int64_t *lists, const float *dis0,
+                           int k, float *D, int64_t *I, int nthreads) {
+    or_search_preassigned_metric(x, n, d, T1, codebook, M, ksub, list_off, codes, ids, nprobe, lists, dis0, k, D, I,
+                                 nthreads, 1, NULL);
 }
 
 /* ---------------- k-means (this build's own training) ---------------- */
@@ -359,8 +430,11 @@ void or_kmeans_update(const float *x, int64_t n, int d, int k, const int64_t *as
     free(cnt);
 }
 
-/* Lloyd k-means, niter rounds of (assign by coarse distance, first argmin; update). */
-void or_kmeans(const float *x, int64_t n, int d, int k, int niter, uint64_t seed, float *cent, int nthreads) {
+/* Lloyd k-means, niter rounds of (assign: first nearest centroid by coarse
+ * distance, or for IP (metric 0) first largest inner product; update). */
+void or_kmeans_metric(const float *x, int64_t n, int d, int k, int niter, uint64_t seed, float *cent, int nthreads,
+                      int metric) {
+    const int ip = metric == 0;
     int64_t *init = (int64_t *)malloc(sizeof(int64_t) * k);
     or_rand_perm_prefix(n, k, seed, init);
     for (int c = 0; c < k; c++) memcpy(cent + (int64_t)c * d, x + init[c] * d, sizeof(float) * d);
@@ -373,13 +447,7 @@ void or_kmeans(const float *x, int64_t n, int d, int k, int niter, uint64_t seed
         for (int64_t i = 0; i < n; i++) {
             const float *xi = x + i * d;
             float xn = or_tree(xi, xi, d, OR_NORM);
-            int best = 0;
-            float bd = 0;
-            for (int c = 0; c < k; c++) {
-                float dd = or_coarse_dis(xi, xn, cent + (int64_t)c * d, cn[c], d);
-                if (c == 0 || dd < bd) { bd = dd; best = c; }
-            }
-            assign[i] = best;
+            assign[i] = or_assign(xi, xn, cent, cn, k, d, ip);
         }
         or_kmeans_update(x, n, d, k, assign, cent);
     }
@@ -387,12 +455,18 @@ void or_kmeans(const float *x, int64_t n, int d, int k, int niter, uint64_t seed
     free(cn);
 }
 
-/* IVF-PQ training: coarse k-means, residuals to the top-1 centroid, then one
- * 2^nbits-centroid k-means per sub-space (seed + 1 + m). */
-void or_train_ivfpq(const float *x, int64_t n, int d, int nlist, int M, int ksub, int niter_coarse,
-                    int niter_pq, uint64_t seed, float *cent, float *codebook, int nthreads) {
+void or_kmeans(const float *x, int64_t n, int d, int k, int niter, uint64_t seed, float *cent, int nthreads) {
+    or_kmeans_metric(x, n, d, k, niter, seed, cent, nthreads, 1);
+}
+
+/* IVF-PQ training: coarse k-means (assignment by the index metric), residuals
+ * to the assigned centroid, then one 2^nbits-centroid L2 k-means per sub-space
+ * (seed + 1 + m; Faiss trains the product quantizer in L2 for both metrics). */
+void or_train_ivfpq_metric(const float *x, int64_t n, int d, int nlist, int M, int ksub, int niter_coarse,
+                           int niter_pq, uint64_t seed, float *cent, float *codebook, int nthreads, int metric) {
     int dsub = d / M;
-    or_kmeans(x, n, d, nlist, niter_coarse, seed, cent, nthreads);
+    const int ip = metric == 0;
+    or_kmeans_metric(x, n, d, nlist, niter_coarse, seed, cent, nthreads, metric);
     float *cn = (float *)malloc(sizeof(float) * nlist);
     or_norms(cent, nlist, d, cn);
     float *r = (float *)malloc(sizeof(float) * n * d);
@@ -400,12 +474,7 @@ void or_train_ivfpq(const float *x, int64_t n, int d, int nlist, int M, int ksub
     for (int64_t i = 0; i < n; i++) {
         const float *xi = x + i * d;
         float xn = or_tree(xi, xi, d, OR_NORM);
-        int best = 0;
-        float bd = 0;
-        for (int c = 0; c < nlist; c++) {
-            float dd = or_coarse_dis(xi, xn, cent + (int64_t)c * d, cn[c], d);
-            if (c == 0 || dd < bd) { bd = dd; best = c; }
-        }
+        int best = or_assign(xi, xn, cent, cn, nlist, d, ip);
         for (int t = 0; t < d; t++) r[i * d + t] = xi[t] - cent[(int64_t)best * d + t];
     }
     float *sub = (float *)malloc(sizeof(float) * n * dsub);
@@ -417,6 +486,11 @@ void or_train_ivfpq(const float *x, int64_t n, int d, int nlist, int M, int ksub
     free(sub);
     free(r);
     free(cn);
+}
+
+void or_train_ivfpq(const float *x, int64_t n, int d, int nlist, int M, int ksub, int niter_coarse,
+                    int niter_pq, uint64_t seed, float *cent, float *codebook, int nthreads) {
+    or_train_ivfpq_metric(x, n, d, nlist, M, ksub, niter_coarse, niter_pq, seed, cent, codebook, nthreads, 1);
 }
 
 /* recall helpers */

@@ -45,6 +45,7 @@ def lib():
         L.or_norms.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p]
         L.or_coarse_search.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, _f32p, ctypes.c_int,
                                        ctypes.c_int, _i64p, _f32p, ctypes.c_int]
+        L.or_coarse_search_metric.argtypes = L.or_coarse_search.argtypes + [ctypes.c_int]
         L.or_ip_table.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
         L.or_precompute_T1.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
         L.or_encode.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, _f32p, ctypes.c_int, _f32p,
@@ -52,11 +53,15 @@ def lib():
         L.or_search_preassigned.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, _f32p, ctypes.c_int,
                                             ctypes.c_int, _i64p, _u8p, _i64p, ctypes.c_int, _i64p, _f32p,
                                             ctypes.c_int, _f32p, _i64p, ctypes.c_int]
+        L.or_search_preassigned_metric.argtypes = L.or_search_preassigned.argtypes + [ctypes.c_int, _f32p]
         L.or_kmeans.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                 _f32p, ctypes.c_int]
         L.or_train_ivfpq.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.c_uint64, _f32p, _f32p, ctypes.c_int]
         L.or_rand_perm_prefix.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, _i64p]
+        L.or_encode_metric.argtypes = L.or_encode.argtypes + [ctypes.c_int]
+        L.or_kmeans_metric.argtypes = L.or_kmeans.argtypes + [ctypes.c_int]
+        L.or_train_ivfpq_metric.argtypes = L.or_train_ivfpq.argtypes + [ctypes.c_int]
     return _LIB
 
 
@@ -111,7 +116,12 @@ def precompute_T1(centroids, codebook):
     return out
 
 
-def coarse_search(x, centroids, nprobe, nthreads=None):
+METRIC_INNER_PRODUCT = 0
+METRIC_L2 = 1
+
+
+def coarse_search(x, centroids, nprobe, nthreads=None, metric=METRIC_L2):
+    """IndexFlatL2 / IndexFlatIP search of the centroids: (dis, lists) [n][nprobe]."""
     x = _f32(x)
     centroids = _f32(centroids)
     cn = norms(centroids)
@@ -120,16 +130,16 @@ def coarse_search(x, centroids, nprobe, nthreads=None):
     nprobe = min(nprobe, nlist)
     lists = np.empty((n, nprobe), np.int64)
     dis = np.empty((n, nprobe), np.float32)
-    lib().or_coarse_search(_p(x, _f32p), n, d, _p(centroids, _f32p), _p(cn, _f32p), nlist, nprobe,
-                           _p(lists, _i64p), _p(dis, _f32p), nthreads or default_threads())
+    lib().or_coarse_search_metric(_p(x, _f32p), n, d, _p(centroids, _f32p), _p(cn, _f32p), nlist, nprobe,
+                                  _p(lists, _i64p), _p(dis, _f32p), nthreads or default_threads(), metric)
     return dis, lists
 
 
-def kmeans(x, k, niter, seed, nthreads=None):
+def kmeans(x, k, niter, seed, nthreads=None, metric=1):
     x = _f32(x)
     out = np.empty((k, x.shape[1]), np.float32)
-    lib().or_kmeans(_p(x, _f32p), x.shape[0], x.shape[1], k, niter, seed, _p(out, _f32p),
-                    nthreads or default_threads())
+    lib().or_kmeans_metric(_p(x, _f32p), x.shape[0], x.shape[1], k, niter, seed, _p(out, _f32p),
+                           nthreads or default_threads(), metric)
     return out
 
 
@@ -140,9 +150,10 @@ def rand_perm_prefix(n, k, seed):
 
 
 class OracleIVFPQ:
-    """CPU IVF-PQ (L2, by_residual, precomputed tables) with Faiss-1.7.1 order."""
+    """CPU IVF-PQ (by_residual; L2 with precomputed tables, or inner product)
+    with Faiss-1.7.1 order."""
 
-    def __init__(self, d, nlist, M, nbits=8):
+    def __init__(self, d, nlist, M, nbits=8, metric=METRIC_L2):
         if nbits != 8:
             raise ValueError("oracle supports nbits=8")
         if d % M:
@@ -156,6 +167,7 @@ class OracleIVFPQ:
         self.list_ids = [np.zeros(0, np.int64) for _ in range(nlist)]
         self.ntotal = 0
         self.nthreads = default_threads()
+        self.metric = metric
 
     @property
     def is_trained(self):
@@ -171,8 +183,8 @@ class OracleIVFPQ:
         x = _f32(x)
         cent = np.empty((self.nlist, self.d), np.float32)
         cb = np.empty((self.M, self.ksub, self.d // self.M), np.float32)
-        lib().or_train_ivfpq(_p(x, _f32p), x.shape[0], self.d, self.nlist, self.M, self.ksub, niter_coarse,
-                             niter_pq, seed, _p(cent, _f32p), _p(cb, _f32p), self.nthreads)
+        lib().or_train_ivfpq_metric(_p(x, _f32p), x.shape[0], self.d, self.nlist, self.M, self.ksub, niter_coarse,
+                                    niter_pq, seed, _p(cent, _f32p), _p(cb, _f32p), self.nthreads, self.metric)
         self.set_trained(cent, cb)
 
     def encode(self, x):
@@ -180,9 +192,9 @@ class OracleIVFPQ:
         n = x.shape[0]
         lists = np.empty(n, np.int64)
         codes = np.empty((n, self.M), np.uint8)
-        lib().or_encode(_p(x, _f32p), n, self.d, _p(self.centroids, _f32p), _p(self.cnorm, _f32p), self.nlist,
-                        _p(self.codebook, _f32p), self.M, self.ksub, _p(lists, _i64p), _p(codes, _u8p),
-                        self.nthreads)
+        lib().or_encode_metric(_p(x, _f32p), n, self.d, _p(self.centroids, _f32p), _p(self.cnorm, _f32p),
+                               self.nlist, _p(self.codebook, _f32p), self.M, self.ksub, _p(lists, _i64p),
+                               _p(codes, _u8p), self.nthreads, self.metric)
         return lists, codes
 
     def add_preencoded(self, lists, codes, ids):
@@ -224,12 +236,13 @@ class OracleIVFPQ:
         off, codes, ids = self.invlists_flat()
         D = np.empty((n, k), np.float32)
         I = np.empty((n, k), np.int64)
-        lib().or_search_preassigned(_p(x, _f32p), n, self.d, _p(self.T1, _f32p), _p(self.codebook, _f32p),
-                                    self.M, self.ksub, _p(off, _i64p), _p(codes, _u8p), _p(ids, _i64p), nprobe,
-                                    _p(lists, _i64p), _p(dis0, _f32p), k, _p(D, _f32p), _p(I, _i64p),
-                                    nthreads or self.nthreads)
+        lib().or_search_preassigned_metric(_p(x, _f32p), n, self.d, _p(self.T1, _f32p), _p(self.codebook, _f32p),
+                                           self.M, self.ksub, _p(off, _i64p), _p(codes, _u8p), _p(ids, _i64p),
+                                           nprobe, _p(lists, _i64p), _p(dis0, _f32p), k, _p(D, _f32p),
+                                           _p(I, _i64p), nthreads or self.nthreads, self.metric,
+                                           _p(self.centroids, _f32p))
         return D, I
 
     def search(self, x, k, nthreads=None):
-        dis, lists = coarse_search(x, self.centroids, self.nprobe, nthreads or self.nthreads)
+        dis, lists = coarse_search(x, self.centroids, self.nprobe, nthreads or self.nthreads, self.metric)
         return self.search_preassigned(x, k, lists, dis, nthreads)

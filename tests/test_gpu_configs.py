@@ -69,6 +69,26 @@ def test_c1_c2_sift1m_shape(sift1m, nprobe):
     assert_same(D, I, Dr, Ir)
 
 
+def test_c2_encode_parity_and_result_shape(sift1m):
+    """GPU add (coarse assignment + PQ encode) equals the oracle's encode on a
+    slice of the base set; results are sorted, with no duplicate labels."""
+    ix, ox, xq = sift1m
+    # the first 20k base vectors (the generator draws in blocks of 65536)
+    xb = datasets.synthetic_sift_like(65_536, 128, seed=1234)[:20_000]
+    lo, co = ox.encode(xb)
+    ids0 = np.concatenate([ix.invlists.get_ids(l) for l in range(ix.nlist)])
+    lists_all = np.concatenate([np.full(ix.invlists.list_size(l), l) for l in range(ix.nlist)])
+    codes_all = np.concatenate([ox.list_codes[l] for l in range(ix.nlist)])
+    sel = ids0 < 20_000
+    o = np.argsort(ids0[sel])
+    np.testing.assert_array_equal(lists_all[sel][o], lo)
+    np.testing.assert_array_equal(codes_all[sel][o], co)
+    ix.nprobe = 16
+    D, I = ix.search(xq, 10)
+    assert np.all(np.diff(D, axis=1) >= 0)
+    assert all(len(set(r.tolist())) == 10 for r in I)
+
+
 def test_c2_k100(sift1m):
     """k = 100, the reference's profiling K (MICRO_GPU_profiling)."""
     ix, ox, xq = sift1m

@@ -60,25 +60,6 @@ def test_search_matches_golden(golden_dir, case):
     assert_same(D, I, z["or_D"], z["or_I"])
 
 
-@pytest.mark.parametrize("scan", ["query", "seedless"])
-@pytest.mark.parametrize("case", CASES)
-def test_alternative_scan_paths_match_golden(golden_dir, case, scan, monkeypatch):
-    """The query-major fused kernel (IVFPQ_SCAN=query) and the list-major path
-    without the threshold-seed pass (IVFPQ_DEBUG=64) give the same results as
-    the default path.  Both switches are read when the index is created."""
-    z = load_case(golden_dir, case)
-    if scan == "query":
-        monkeypatch.setenv("IVFPQ_SCAN", "query")
-    else:
-        monkeypatch.setenv("IVFPQ_DEBUG", "64")
-    ix = gpu_index(z)
-    for k in (int(z["k"]), 100):
-        ox = oracle_index(z)
-        Dr, Ir = ox.search(z["xq"], k)
-        D, I = ix.search(z["xq"], k)
-        assert_same(D, I, Dr, Ir)
-
-
 @pytest.mark.parametrize("case", CASES)
 def test_coarse_and_tables_match_oracle(golden_dir, case):
     import torch
@@ -242,6 +223,52 @@ def test_device_entry_points_match_host(golden_dir):
     assert_same(D2.cpu().numpy(), I2.cpu().numpy(), z["or_D"], z["or_I"])
 
 
+def test_device_searches_on_two_streams_without_sync(golden_dir):
+    """Two device searches on different streams and then a host search(), with
+    no synchronisation in between: the library orders them on the handle's
+    shared workspaces (bucket counters, partial lists, T3), so all three are
+    bit-exact."""
+    import torch
+
+    z = load_case(golden_dir, "d128_m16")
+    ix = gpu_index(z)
+    xq = torch.from_numpy(z["xq"]).cuda()
+    xr = torch.flip(xq, dims=[0]).contiguous()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for rep in range(3):
+        with torch.cuda.stream(s1):
+            D1, I1 = ix.search_device(xq, 10)
+        with torch.cuda.stream(s2):
+            D2, I2 = ix.search_device(xr, 10)
+        D3, I3 = ix.search(z["xq"], 10)
+        outs.append((D1, I1, D2, I2, D3, I3))
+    torch.cuda.synchronize()
+    for D1, I1, D2, I2, D3, I3 in outs:
+        assert_same(D1.cpu().numpy(), I1.cpu().numpy(), z["or_D"], z["or_I"])
+        assert_same(D2.cpu().numpy(), I2.cpu().numpy(), z["or_D"][::-1], z["or_I"][::-1])
+        assert_same(D3, I3, z["or_D"], z["or_I"])
+
+
+def test_device_entry_points_reject_bad_tensors(golden_dir):
+    import torch
+
+    z = load_case(golden_dir, "d128_m16")
+    ix = gpu_index(z)
+    xq = torch.from_numpy(z["xq"]).cuda()
+    for bad in (xq.half(), xq[:, :64], xq.t(), xq.cpu(), xq[:, ::2]):
+        with pytest.raises(RuntimeError):
+            ix.search_device(bad, 10)
+    with pytest.raises(RuntimeError):
+        ix.search_device(xq, 10, D=torch.empty((3, 10), device="cuda"))
+    Dq, Iq = ix.coarse_device(xq)
+    with pytest.raises(RuntimeError):
+        ix.search_preassigned_device(xq, 10, Iq.int(), Dq)
+    with pytest.raises(RuntimeError):
+        ix.search_preassigned_device(xq, 10, Iq[:, :3].contiguous(), None)
+
+
 def test_merge_topk_device():
     import torch
 
@@ -318,44 +345,3 @@ def test_errors_are_runtime_errors(golden_dir):
         faiss.IndexIVFPQ(None, 128, 64, 16, 8, device=0).search(z["xq"], 5)  # untrained
     with pytest.raises(RuntimeError):
         faiss.IndexIVFPQ(None, 100, 64, 16, 8, device=0)  # d % M != 0
-
-
-def test_c2_full_size_bit_exact():
-    """C2 shape (SIFT1M-like, nlist=1024, M=16, nprobe=16, batch 1024): the GPU
-    engine's result equals the oracle's on the same trained index, and the
-    result is sorted with no duplicate labels."""
-    xt = datasets.synthetic_sift_like(100_000, 128, seed=4321)
-    xb = datasets.synthetic_sift_like(1_000_000, 128, seed=1234)
-    xq = datasets.synthetic_sift_like(1024, 128, seed=123)
-    ix = faiss.index_factory(128, "IVF1024,PQ16")
-    ix.niter_coarse, ix.niter_pq = 8, 8
-    ix.train(xt)
-    ix.add(xb)
-    ix.nprobe = 16
-    D, I = ix.search(xq, 10)
-    ox = O.OracleIVFPQ(128, 1024, 16)
-    ox.set_trained(ix.centroids(), ix.codebook())
-    # encode parity on a slice of the base set
-    lo, co = ox.encode(xb[:20000])
-    ids0 = np.concatenate([ix.invlists.get_ids(l) for l in range(1024)])
-    assert ids0.shape[0] == 1_000_000
-    for l in range(1024):
-        ox.list_ids[l] = ix.invlists.get_ids(l)
-        ox.list_codes[l] = ix.invlists.get_codes(l).reshape(-1, 16)
-    ox.ntotal = ix.ntotal
-    sel = ids0 < 20000
-    lists_all = np.concatenate([np.full(ix.invlists.list_size(l), l) for l in range(1024)])
-    codes_all = np.concatenate([ox.list_codes[l] for l in range(1024)])
-    o = np.argsort(ids0[sel])
-    np.testing.assert_array_equal(lists_all[sel][o], lo)
-    np.testing.assert_array_equal(codes_all[sel][o], co)
-    ox.nprobe = 16
-    Dr, Ir = ox.search(xq, 10)
-    assert_same(D, I, Dr, Ir)
-    assert np.all(np.diff(D, axis=1) >= 0)
-    for q in range(I.shape[0]):
-        assert len(set(I[q].tolist())) == 10
-    for k in (100, 1000):
-        D, I = ix.search(xq[:256], k)
-        Dr, Ir = ox.search(xq[:256], k)
-        assert_same(D, I, Dr, Ir)

@@ -137,3 +137,50 @@ def test_padding_fewer_than_k():
     D, I = ox.search(rng.standard_normal((3, 16)).astype(np.float32), 8)
     assert np.all(I[:, 5:] == -1)
     assert np.all(D[:, 5:] == np.finfo(np.float32).max)
+
+
+def test_oracle_inner_product_semantics():
+    """METRIC_INNER_PRODUCT (beir/beir/retrieval/search/dense/faiss_search.py:170,
+    194), checked against a direct restatement on integer-valued data (every
+    product and sum is exact, so only the semantics are under test): coarse =
+    the nprobe largest <q, c>; dis0 = <q, c_l>; LUT = T3; the k largest
+    dis0 + sum_m T3[m][code_m], descending, ties by label; padding (-FLT_MAX, -1).
+    Parity with Faiss itself is unpinned (the reference's oracle is L2-only)."""
+    rng = np.random.default_rng(7)
+    d, M, nlist, nprobe, k = 16, 4, 8, 3, 7
+    cent = rng.integers(-3, 4, size=(nlist, d)).astype(np.float32)
+    cb = rng.integers(-3, 4, size=(M, 256, d // M)).astype(np.float32)
+    ox = O.OracleIVFPQ(d, nlist, M, metric=O.METRIC_INNER_PRODUCT)
+    ox.set_trained(cent, cb)
+    nb = 300
+    lists = rng.integers(0, nlist, size=nb).astype(np.int64)
+    lists[lists == 5] = 4  # list 5 stays empty
+    codes = rng.integers(0, 256, size=(nb, M)).astype(np.uint8)
+    codes[10:40] = codes[0]  # exact ties
+    ids = rng.permutation(nb).astype(np.int64) * 3
+    ox.add_preencoded(lists, codes, ids)
+    ox.nprobe = nprobe
+    xq = rng.integers(-3, 4, size=(6, d)).astype(np.float32)
+    D, I = ox.search(xq, k)
+    dsub = d // M
+    for q in range(xq.shape[0]):
+        x = xq[q].astype(np.float64)
+        sims = cent.astype(np.float64) @ x
+        probes = sorted(range(nlist), key=lambda l: (-sims[l], l))[:nprobe]
+        t3 = np.einsum("mjt,mt->mj", cb.astype(np.float64), x.reshape(M, dsub))
+        cand = []
+        for l in probes:
+            for i in np.where(lists == l)[0]:
+                cand.append((sims[l] + sum(t3[m, codes[i, m]] for m in range(M)), ids[i]))
+        cand.sort(key=lambda t: (-t[0], t[1]))
+        cand = cand[:k]
+        exp_I = [c[1] for c in cand] + [-1] * (k - len(cand))
+        exp_D = [c[0] for c in cand] + [-np.finfo(np.float32).max] * (k - len(cand))
+        np.testing.assert_array_equal(I[q], exp_I)
+        np.testing.assert_array_equal(D[q], np.array(exp_D, np.float32))
+    dis, lst = O.coarse_search(xq, cent, nprobe, metric=O.METRIC_INNER_PRODUCT)
+    assert np.all(np.diff(dis, axis=1) <= 0)
+    # preassigned: the coarse similarities passed in are not used (dis0 is recomputed)
+    D2, I2 = ox.search_preassigned(xq, k, lst, np.zeros_like(dis))
+    np.testing.assert_array_equal(I2, I)
+    np.testing.assert_array_equal(D2, D)
