@@ -73,7 +73,7 @@ struct ListPlan {
   int2* bucket;      // [nloc][2 kinds][cap] (pair id q*nprobe+p, dis0 key bits)
   int cap;           // bucket slots per list (>= queries in the batch)
   int32_t* recs;     // [max_items][16] work items: list, count, size, beg(2), pairs[4], dis0[4]
-  int32_t* hdr;      // [16]: n_items, n_items of kind 0, 8 per-XCD-group work counters
+  int32_t* hdr;      // [16]: n_items, n_items of kind 0, the list scan's work counter, 0...
   int max_items;
   float* partD;      // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k (keys)
   int64_t* partI;    // same shape: global code positions (-1 = none)

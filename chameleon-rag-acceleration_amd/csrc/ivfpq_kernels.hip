@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include <hip/hip_runtime.h>
 
@@ -95,7 +96,8 @@ __device__ __forceinline__ float tree(FX fx, FY fy, int d) {
   return h0 + h1;
 }
 
-__device__ __forceinline__ bool lexless(float ad, int64_t ai, float bd, int64_t bi) {
+template <class T>
+__device__ __forceinline__ bool lexless(float ad, T ai, float bd, T bi) {
   return ad < bd || (ad == bd && ai < bi);
 }
 
@@ -103,24 +105,11 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-__device__ __forceinline__ int64_t readlane_i64(int64_t v, int lane) {
-  const uint64_t u = (uint64_t)v;
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
 // Cross-lane moves on the VALU (DPP) instead of the LDS crossbar (ds_bpermute):
 // wave_shr:1 shifts the whole wave by one lane, lane 0 receiving `old`.
 __device__ __forceinline__ int dpp_shr1_i(int old, int v) { return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false); }
 __device__ __forceinline__ float shr1_f(float old, float v) {
   return __int_as_float(dpp_shr1_i(__float_as_int(old), __float_as_int(v)));
-}
-__device__ __forceinline__ int64_t shr1_i64(int64_t old, int64_t v) {
-  const uint64_t uo = (uint64_t)old, uv = (uint64_t)v;
-  const uint32_t lo = (uint32_t)dpp_shr1_i((int)(uint32_t)uo, (int)(uint32_t)uv);
-  const uint32_t hi = (uint32_t)dpp_shr1_i((int)(uint32_t)(uo >> 32), (int)(uint32_t)(uv >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // lane ^ J exchange: DPP for J <= 8, ds_swizzle for 16, bpermute for 32
@@ -139,32 +128,63 @@ __device__ __forceinline__ int xor_i(int v) {
 }
 template <int J>
 __device__ __forceinline__ float xor_f(float v) { return __int_as_float(xor_i<J>(__float_as_int(v))); }
+
+// Candidate ids: int64 labels / global positions, or int32 positions inside one
+// list (the list scan): half the cross-lane traffic of the top-k network.
+__device__ __forceinline__ int id_readlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ int64_t id_readlane(int64_t v, int lane) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int id_shr1(int old, int v) { return dpp_shr1_i(old, v); }
+__device__ __forceinline__ int64_t id_shr1(int64_t old, int64_t v) {
+  const uint64_t uo = (uint64_t)old, uv = (uint64_t)v;
+  const uint32_t lo = (uint32_t)dpp_shr1_i((int)(uint32_t)uo, (int)(uint32_t)uv);
+  const uint32_t hi = (uint32_t)dpp_shr1_i((int)(uint32_t)(uo >> 32), (int)(uint32_t)(uv >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 template <int J>
-__device__ __forceinline__ int64_t xor_i64(int64_t v) {
+__device__ __forceinline__ int id_xor(int v) { return xor_i<J>(v); }
+template <int J>
+__device__ __forceinline__ int64_t id_xor(int64_t v) {
   const uint64_t u = (uint64_t)v;
   const uint32_t lo = (uint32_t)xor_i<J>((int)(uint32_t)u);
   const uint32_t hi = (uint32_t)xor_i<J>((int)(uint32_t)(u >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+__device__ __forceinline__ int id_shfl(int v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ int64_t id_shfl(int64_t v, int src) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), src, 64);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <class T>
+__device__ __forceinline__ constexpr T id_none() {
+  if constexpr (sizeof(T) == 8) return (T)kSentinelId;
+  else return (T)INT32_MAX;
+}
 
-// A wave's running k best (dist, label) pairs, sorted ascending across
+// A wave's running k best (key, id) pairs, sorted ascending across
 // R rows x 64 lanes (logical index r*64 + lane).  Requires k <= 64*R.
-template <int R>
+template <int R, class T = int64_t>
 struct WaveTopK {
   float d[R];
-  int64_t id[R];
-  float td;     // current k-th best (the admission threshold)
-  int64_t ti;
+  T id[R];
+  float td;  // current k-th best (the admission threshold)
+  T ti;
   int krow, klane;
 
   __device__ __forceinline__ void init(int k) {
 #pragma unroll
     for (int r = 0; r < R; r++) {
       d[r] = kInf;
-      id[r] = kSentinelId;
+      id[r] = id_none<T>();
     }
     td = kInf;
-    ti = kSentinelId;
+    ti = id_none<T>();
     krow = (k - 1) >> 6;
     klane = (k - 1) & 63;
   }
@@ -174,18 +194,18 @@ struct WaveTopK {
     for (int r = 0; r < R; r++) {
       if (r == krow) {
         td = readlane_f(d[r], klane);
-        ti = readlane_i64(id[r], klane);
+        ti = id_readlane(id[r], klane);
       }
     }
   }
 
   // Insert the candidates (cd, ci) of the lanes set in `mask` (wave-uniform).
-  __device__ __forceinline__ void insert(uint64_t mask, float cd, int64_t ci, int lane) {
+  __device__ __forceinline__ void insert(uint64_t mask, float cd, T ci, int lane) {
     while (mask) {
       const int src = __builtin_ctzll(mask);
       mask &= mask - 1;
       const float vd = readlane_f(cd, src);
-      const int64_t vi = readlane_i64(ci, src);
+      const T vi = id_readlane(ci, src);
       if (!lexless(vd, vi, td, ti)) continue;  // overtaken by an earlier insert
       int pos = 0;
 #pragma unroll
@@ -194,13 +214,13 @@ struct WaveTopK {
       for (int r = R - 1; r >= 0; r--) {
         if ((r + 1) * 64 <= pos) continue;  // row entirely before the slot
         float cdd = vd;
-        int64_t cii = vi;
+        T cii = vi;
         if (r > 0) {
           cdd = readlane_f(d[r - 1], 63);
-          cii = readlane_i64(id[r - 1], 63);
+          cii = id_readlane(id[r - 1], 63);
         }
         const float ud = shr1_f(cdd, d[r]);
-        const int64_t ui = shr1_i64(cii, id[r]);
+        const T ui = id_shr1(cii, id[r]);
         const int idx = r * 64 + lane;
         if (idx > pos) {
           d[r] = ud;
@@ -215,22 +235,14 @@ struct WaveTopK {
   }
 };
 
-__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
-  const uint64_t u = (uint64_t)v;
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, src, 64);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), src, 64);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
-
 // Merge up to 64 candidates (one per lane; (inf, sentinel) = none) into a
 // single-row top-k: bitonic sort of the candidates, then the classic
 // reverse-min + bitonic merge against the sorted row.  Exchanges at strides
 // <= 8 are DPP moves, 16 a ds_swizzle, 32 a bpermute.
-template <int KK, int J>
-__device__ __forceinline__ void bitonic_step(float& cd, int64_t& ci, int lane) {
+template <int KK, int J, class T>
+__device__ __forceinline__ void bitonic_step(float& cd, T& ci, int lane) {
   const float od = xor_f<J>(cd);
-  const int64_t oi = xor_i64<J>(ci);
+  const T oi = id_xor<J>(ci);
   const bool up = (lane & KK) == 0;
   const bool lower = (lane & J) == 0;
   const bool take = (lower == up) ? lexless(od, oi, cd, ci) : lexless(cd, ci, od, oi);
@@ -239,25 +251,26 @@ __device__ __forceinline__ void bitonic_step(float& cd, int64_t& ci, int lane) {
     ci = oi;
   }
 }
-template <int KK, int J>
-__device__ __forceinline__ void bitonic_steps(float& cd, int64_t& ci, int lane) {
+template <int KK, int J, class T>
+__device__ __forceinline__ void bitonic_steps(float& cd, T& ci, int lane) {
   if constexpr (J >= 1) {
     bitonic_step<KK, J>(cd, ci, lane);
     bitonic_steps<KK, J / 2>(cd, ci, lane);
   }
 }
-template <int KK>
-__device__ __forceinline__ void bitonic_sort64(float& cd, int64_t& ci, int lane) {
+template <int KK, class T>
+__device__ __forceinline__ void bitonic_sort64(float& cd, T& ci, int lane) {
   if constexpr (KK <= 64) {
     bitonic_steps<KK, KK / 2>(cd, ci, lane);
     bitonic_sort64<KK * 2>(cd, ci, lane);
   }
 }
 
-__device__ __forceinline__ void bulk_merge_row(WaveTopK<1>& tk, float cd, int64_t ci, int lane) {
+template <class T>
+__device__ __forceinline__ void bulk_merge_row(WaveTopK<1, T>& tk, float cd, T ci, int lane) {
   bitonic_sort64<2>(cd, ci, lane);
   const float rd = __shfl(cd, 63 - lane, 64);
-  const int64_t ri = shfl_i64(ci, 63 - lane);
+  const T ri = id_shfl(ci, 63 - lane);
   if (lexless(rd, ri, tk.d[0], tk.id[0])) {
     tk.d[0] = rd;
     tk.id[0] = ri;
@@ -308,7 +321,7 @@ __device__ __forceinline__ void lane_sort(float (&d)[KL], int64_t (&id)[KL]) {
 template <int J>
 __device__ __forceinline__ void min_step(float& d, int64_t& id) {
   const float od = xor_f<J>(d);
-  const int64_t oi = xor_i64<J>(id);
+  const int64_t oi = id_xor<J>(id);
   if (lexless(od, oi, d, id)) {
     d = od;
     id = oi;
@@ -1076,36 +1089,52 @@ struct CodeWords {
 
 template <int G>
 struct Item {
-  int l, cnt, n;
+  int l, cnt, n, kind;
   int64_t beg;
   int pair[G];
   float d0[G];
 };
 
-// Persistent workgroups walk the work items: a workgroup starts in its XCD
-// group's chunk (blocks b and b + 8 share an XCD, so the consecutive items of
-// one list -- same T1 row, same codes -- stay on one L2), kind-0 items first,
-// then helps the other groups.  A work item is (list l, up to G pairs): the G
-// LUTs are interleaved per entry ([m][j][g]) so one ds_read_b{32,64,128}
-// returns the G lookups of a code and the bank conflicts of the random 8-bit
-// gathers are paid once per G lookups.  PF: the next item's record and T1/T3
-// rows are loaded into registers while the current item is scanned, so the
-// LUT build after the barrier never waits on memory.
-// Candidates (key <= min(own k-th, tau_q)) go to a per-wave LDS queue that one
-// compact loop drains into the wave's per-query top-k, ranked by (key, code
-// position): device lists are label-sorted, so this equals (key, label) inside
-// a list.  tau_q is shared across workgroups through global atomicMin (any k
-// real candidates bound the final k-th; a stale read is only a looser bound).
+// Persistent workgroups take work items from one counter: kind-0 items (each
+// query's first probe) first, so that a query's running k-th key tau_q is
+// usually known before its other probes are scanned.  A work item is (list l,
+// up to G pairs): the G LUTs are interleaved per entry ([m][j][g]) so one
+// ds_read_b{32,64,128} returns the G lookups of a code and the bank conflicts
+// of the random 8-bit gathers are paid once per G lookups.
+// Per item: the item's codes (up to JB chunks of 256 codes) are loaded together
+// with the LUT rows -- one memory round trip -- and the next item index is
+// fetched at the same time; then the codes are gathered one chunk (64 codes
+// per wave) at a time.  Candidates (key <= min(own k-th, tau_q)) go to a
+// per-wave LDS queue that one compact loop drains into the wave's per-query
+// top-k, ranked by (key, position in the list): device lists are
+// label-sorted, so this equals (key, label) inside a list.  While a query has
+// no bound yet the queue is drained after every chunk.  tau_q is shared
+// across workgroups through global atomicMin (any k real candidates bound the
+// final k-th; a stale read is only a looser bound).
 constexpr int QCAP = 256;  // per-wave candidate queue entries
 
-template <int M, int G, int R, int J, bool PF>
+#ifdef DIAG_STAMPS  // diagnostic builds only (profiles/diag_stamps.py): per-item phase stamps
+constexpr int kDiagWG = 1024, kDiagItems = 64, kDiagSlots = 8;
+__device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
+#define DIAG(slot, v)                                                                                \
+  do {                                                                                               \
+    if (tid == 0 && blockIdx.x < kDiagWG && it_no < kDiagItems)                                      \
+      g_diag[((size_t)blockIdx.x * kDiagItems + it_no) * kDiagSlots + (slot)] = (uint64_t)(v);        \
+  } while (0)
+#else
+#define DIAG(slot, v) \
+  do {                \
+  } while (0)
+#endif
+
+template <int M, int G, int R, int JB>
 __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) {
   using V = typename LutVec<G>::T;
   constexpr int LUTN = M * 256;
   constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table
   __shared__ __attribute__((aligned(16))) V lut[LUTN];
   __shared__ float qd[4][QCAP];
-  __shared__ int32_t qi[4][QCAP];  // (code position << 2) | g
+  __shared__ int32_t qi[4][QCAP];  // (position in the list << 2) | g
   __shared__ int s_next;
 
   const int tid = threadIdx.x;
@@ -1116,34 +1145,18 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   const int nloc = a.list_hi - a.list_lo;
   if (blockIdx.x == 0)  // the counts were consumed by k_plan_items: zero them for the next batch
     for (int i = tid; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
-  const int n_items = pl.hdr[0], N0 = pl.hdr[1], N1 = n_items - N0;
-  const int per0 = (N0 + 7) >> 3, per1 = (N1 + 7) >> 3;
-  const int grp = blockIdx.x & 7;
-  int ngv = 0;  // groups exhausted so far (thread 0)
-  auto fetch = [&]() -> int {
-    while (ngv < 8) {
-      const int g = (grp + ngv) & 7;
-      const int a0 = g * per0, n0g = max(0, min(N0, a0 + per0) - a0);
-      const int a1 = g * per1, n1g = max(0, min(N1, a1 + per1) - a1);
-      const int t = atomicAdd(pl.hdr + 2 + g, 1);
-      if (t < n0g) return a0 + t;
-      if (t < n0g + n1g) return N0 + a1 + (t - n0g);
-      ngv++;
-    }
-    return -1;
-  };
+  const int n_items = pl.hdr[0];
   const uint64_t lanemask_lt = (1ull << lane) - 1;
 
   Item<G> it;
-  float4 t1v[PF ? NV : 1];
-  float4 t3v[G][PF ? NV : 1];
-  auto load_item = [&](int idx) {
+  auto load_item = [&](int idx) __attribute__((always_inline)) {
     const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)__builtin_amdgcn_readfirstlane(idx) * 16);
     const int4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
     it.l = r0.x;
     it.cnt = r0.y;
     it.n = r0.z;
     it.beg = (int64_t)(((uint64_t)(uint32_t)r1.x << 32) | (uint32_t)r0.w);
+    it.kind = r3.y;
     const int pr[4] = {r1.y, r1.z, r1.w, r2.x};
     const int db[4] = {r2.y, r2.z, r2.w, r3.x};
 #pragma unroll
@@ -1152,52 +1165,31 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       it.d0[g] = __int_as_float(db[g]);
     }
   };
-  auto load_tables = [&](bool need_t1) {  // PF only
-    if constexpr (PF) {
-      if (need_t1 && !ip) {
-        const float4* T1l = reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
-#pragma unroll
-        for (int e = 0; e < NV; e++) t1v[e] = T1l[e * 256 + tid];
-      }
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if (g < it.cnt) {
-          const float4* T3q = reinterpret_cast<const float4*>(a.T3 + (int64_t)(it.pair[g] / a.nprobe) * LUTN);
-#pragma unroll
-          for (int e = 0; e < NV; e++) t3v[g][e] = T3q[e * 256 + tid];
-        }
-      }
-    }
-  };
 
-  if (tid == 0) s_next = fetch();
+  if (tid == 0) {
+    const int t = atomicAdd(pl.hdr + 2, 1);
+    s_next = t < n_items ? t : -1;
+  }
   __syncthreads();
   int cur = s_next;
-  if (cur >= 0) {
-    load_item(cur);
-    if constexpr (PF) load_tables(true);
-  }
+  if (cur >= 0) load_item(cur);
+  int it_no = 0;
+  (void)it_no;
   while (cur >= 0) {
     __syncthreads();  // (A) every wave is done with the LUT of the previous item, and has read s_next
-    if (tid == 0) s_next = fetch();
-    // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
-    if constexpr (PF) {  // from the rows prefetched into registers
+    DIAG(0, __builtin_amdgcn_s_memtime());
+    int tnext = 0;
+    if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);  // the next item; consumed after the LUT build
+    // the item's first JB x 256 codes, issued with the LUT rows (one round trip for both)
+    const int n = it.n;
+    const uint8_t* lc = a.codes + it.beg * M;
+    CodeWords<M> cw[JB];
 #pragma unroll
-      for (int e = 0; e < NV; e++) {
-        const int v = e * 256 + tid;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          V o;
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            const float t3 = comp(t3v[g][e], c);
-            const float lv = ip ? -t3 : comp(t1v[e], c) + (-2.0f * t3);
-            setc(o, g, g < it.cnt ? lv : 0.f);
-          }
-          lut[4 * v + c] = o;
-        }
-      }
-    } else {  // straight from memory, one float4 of each row at a time
+    for (int j = 0; j < JB; j++) {
+      const int i = j * 256 + wave * 64 + lane;
+      cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
+    }
+    {  // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
       const float4* T1l = reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
       const float4* T3q[G];
 #pragma unroll
@@ -1223,43 +1215,42 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         }
       }
     }
+    if (tid == 0) s_next = tnext < n_items ? tnext : -1;
     __syncthreads();  // (B) the LUT and s_next are visible
+    DIAG(1, __builtin_amdgcn_s_memtime());
     const Item<G> ci = it;
     const int nxt = s_next;
-    const int n = ci.n;
-    const uint8_t* lc = a.codes + ci.beg * M;
-    CodeWords<M> cw[J];
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      const int i = j * 256 + wave * 64 + lane;
-      cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
-    }
-    if constexpr (PF) {
-      if (nxt >= 0) {
-        load_item(nxt);
-        load_tables(it.l != ci.l);  // a run of items of one list keeps its T1 row
-      }
-    }
     int64_t qix[G];
     float bound[G];
+    bool loose = false;  // some query of the item has no bound yet
 #pragma unroll
     for (int g = 0; g < G; g++) {
       qix[g] = (g < ci.cnt ? ci.pair[g] : 0) / a.nprobe;
       bound[g] = g < ci.cnt ? ord2f(pl.tauq[qix[g]]) : -kInf;
+      loose = loose || bound[g] == kInf;
     }
 
-    WaveTopK<R> tk[G];
+    WaveTopK<R, int> tk[G];
 #pragma unroll
     for (int g = 0; g < G; g++) tk[g].init(k);
     int qn = 0;  // this wave's queue fill (wave-uniform)
+#ifdef DIAG_STAMPS
+    int npush = 0;
+#ifdef DIAG_FINE
+    asm volatile("" ::"v"(bound[0]), "v"(bound[G - 1]));
+    DIAG(6, __builtin_amdgcn_s_memtime());
+#else
+    DIAG(7, (uint32_t)f2ord(bound[0]));
+#endif
+#endif
 
     // drain the queue into the per-query top-k lists and publish the bounds
-    auto drain = [&]() {
+    auto drain = [&]() __attribute__((always_inline)) {
       for (int b0 = 0; b0 < qn; b0 += 64) {
         const int e = b0 + lane;
         const float cd = e < qn ? qd[wave][e] : kInf;
         const int cidx = e < qn ? qi[wave][e] : 0;
-        const int64_t pos = cidx >> 2;
+        const int pos = cidx >> 2;
         const int cg = cidx & 3;
 #pragma unroll
         for (int g = 0; g < G; g++) {
@@ -1268,7 +1259,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
           if (mk) {
             if constexpr (R == 1) {
               if (__popcll(mk) > 6)
-                bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : kSentinelId, lane);
+                bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : id_none<int>(), lane);
               else
                 tk[g].insert(mk, cd, pos, lane);
             } else {
@@ -1279,77 +1270,114 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         }
       }
       qn = 0;
+      loose = false;
 #pragma unroll
       for (int g = 0; g < G; g++) {
+        loose = loose || bound[g] == kInf;
         if (g < ci.cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td));
       }
     };
-    auto push = [&](bool pass, uint64_t mask, float dv, int i, int g) {
-      if (pass) {
-        const int sl = qn + __popcll(mask & lanemask_lt);
-        qd[wave][sl] = dv;
-        qi[wave][sl] = (i << 2) | g;
-      }
-      qn += __popcll(mask);
-    };
 
-    for (int base = 0; base < n; base += 256 * J) {
-      if (base > 0) {
+    // Chunks of 64 codes per wave (256 per workgroup), JB of them held in
+    // registers.  The chunks run as a straight sequence of guarded blocks
+    // (compile-time register indices, no selection network) that stops where
+    // the queue needs draining; one drain site serves every stop.
+    for (int sb = 0; sb < n; sb += 256 * JB) {
+      if (sb > 0) {
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-          const int i = base + j * 256 + wave * 64 + lane;
+        for (int j = 0; j < JB; j++) {
+          const int i = sb + j * 256 + wave * 64 + lane;
           cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
         }
       }
-      // all J x G keys first, m-outer: J independent LDS gathers in flight per
-      // step and no control flow between them (per-chain order is the
-      // sequential m order of the oracle)
-      float dis[J][G];
-#pragma unroll
-      for (int j = 0; j < J; j++)
-#pragma unroll
-        for (int g = 0; g < G; g++) dis[j][g] = ci.d0[g];
-#pragma unroll
-      for (int m = 0; m < M; m++) {
-#pragma unroll
-        for (int j = 0; j < J; j++) {
-          const V v = lut[m * 256 + cw[j].byte(m)];
-#pragma unroll
-          for (int g = 0; g < G; g++) dis[j][g] = dis[j][g] + comp(v, g);
-        }
+      const int tn = min(JB, (n - sb + 255) >> 8);  // chunks with codes (wave-uniform)
+#ifdef DIAG_FINE
+      if (sb == 0) {
+        asm volatile("" ::"v"(cw[0].w[0]), "v"(cw[JB - 1].w[0]));
+        DIAG(7, __builtin_amdgcn_s_memtime());
       }
-      // push the J chunks' candidates while they fit; otherwise drain (which
-      // also tightens the bounds) and resume.  One drain site keeps code size down.
-      int jj = 0;
+#endif
+      const bool last_sb = sb + 256 * JB >= n;
+      int t = 0;
       while (true) {
-        int jstop = J;
+        int stop = tn;       // first chunk not yet admitted
+        bool want = false;   // drain requested
+        // one chunk: G keys per code (dis0 + sum_m LUT[m][code_m], sequential in
+        // m: the oracle's order), then admission into the queue
+        auto chunk = [&](int j, const CodeWords<M>& c0) __attribute__((always_inline)) -> bool {
+          // opaque copy of the words: keeps the LUT addresses of all JB chunks from
+          // being hoisted out of the restart loop (128 live VGPRs at JB = 8)
+          CodeWords<M> c = c0;
 #pragma unroll
-        for (int j = 0; j < J; j++) {
-          if (j >= jj && jstop == J) {  // wave-uniform
-            const int i = base + j * 256 + wave * 64 + lane;
-            const bool valid = i < n;
-            uint64_t mk[G];
-            int tj = 0;
+          for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(c.w[v]));
+          const int i = sb + j * 256 + wave * 64 + lane;
+          float dis[G];
 #pragma unroll
-            for (int g = 0; g < G; g++) {
-              mk[g] = __ballot(valid && dis[j][g] <= bound[g]);
-              tj += __popcll(mk[g]);
+          for (int g = 0; g < G; g++) dis[g] = ci.d0[g];
+#pragma unroll
+          for (int m = 0; m < M; m++) {
+#ifdef DIAG_NOGATHER
+            V v;
+            for (int g = 0; g < G; g++) setc(v, g, __int_as_float(c.byte(m)));
+#else
+            const V v = lut[m * 256 + c.byte(m)];
+#endif
+#pragma unroll
+            for (int g = 0; g < G; g++) dis[g] = dis[g] + comp(v, g);
+          }
+          const bool valid = i < n;
+          uint64_t mk[G];
+          int tj = 0;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            mk[g] = __builtin_amdgcn_ballot_w64(valid && dis[g] <= bound[g]);
+            tj += __popcll(mk[g]);
+          }
+          if (tj == 0) return false;
+          if (qn + tj > QCAP) {  // no room: drain first, then redo this chunk
+            stop = j;
+            want = true;
+            return true;
+          }
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if ((mk[g] >> lane) & 1) {
+              const int sl = qn + __popcll(mk[g] & lanemask_lt);
+              qd[wave][sl] = dis[g];
+              qi[wave][sl] = (i << 2) | g;
             }
-            if (qn + tj > QCAP) {
-              jstop = j;
-            } else {
+            qn += __popcll(mk[g]);
+          }
+#ifdef DIAG_STAMPS
+          npush += tj;
+#endif
+          if (loose) {  // a query of the item has no bound yet: get one now
+            stop = j + 1;
+            want = true;
+            return true;
+          }
+          return false;
+        };
+        bool go = true;
 #pragma unroll
-              for (int g = 0; g < G; g++) push((mk[g] >> lane) & 1, mk[g], dis[j][g], i, g);
-            }
+        for (int j = 0; j < JB; j++) {
+          if (go && j >= t && j < tn) {  // wave-uniform guards: a straight sequence of chunks
+            if (chunk(j, cw[j])) go = false;
           }
         }
-        if (jstop == J && qn < QCAP / 2) break;
-        drain();
-        if (jstop == J) break;
-        jj = jstop;
+        if (want || (stop >= tn && last_sb && qn > 0)) drain();
+        if (stop >= tn) break;
+        t = stop;
       }
     }
-    if (qn > 0) drain();
+    DIAG(2, __builtin_amdgcn_s_memtime());
+#ifdef DIAG_STAMPS
+    DIAG(4, n);
+    DIAG(5, ci.cnt | (ci.kind << 8));
+#ifndef DIAG_FINE
+    DIAG(6, npush);
+#endif
+#endif
 
     // each wave writes its own sorted partial list per pair (merged by k_merge_probes)
 #pragma unroll
@@ -1360,15 +1388,15 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       for (int r = 0; r < R; r++) {
         const int ix = r * 64 + lane;
         if (ix < k) {
-          const bool empty = tk[g].id[r] == kSentinelId;
+          const bool empty = tk[g].id[r] == id_none<int>();
           pl.partD[o + ix] = empty ? FLT_MAX : tk[g].d[r];
           pl.partI[o + ix] = empty ? -1 : ci.beg + tk[g].id[r];  // global code position
         }
       }
     }
-    if constexpr (!PF) {
-      if (nxt >= 0) load_item(nxt);
-    }
+    if (nxt >= 0) load_item(nxt);
+    DIAG(3, __builtin_amdgcn_s_memtime());
+    it_no++;
     cur = nxt;
   }
 }
@@ -1663,7 +1691,10 @@ int scan_lists_grid() {
   if (!grid) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = std::max(8, (2 * cus + 7) / 8 * 8);
+#ifndef SCAN_WG_PER_CU
+#define SCAN_WG_PER_CU 2
+#endif
+    grid = std::max(8, (SCAN_WG_PER_CU * cus + 7) / 8 * 8);
   }
   return grid;
 }
@@ -1671,11 +1702,13 @@ int scan_lists_grid() {
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 8) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 8) ? 2 : 1;
-  constexpr int J = M <= 8 ? 8 : M <= 16 ? 4 : 2;  // codes per lane per batch (register budget)
-  constexpr int NV = M / 4;
-  constexpr bool PF = NV * (G + 1) <= 24 && R <= 2;  // register prefetch of the next item's tables
+  constexpr int JB = M <= 16 ? 8 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs)
   if (ev) (void)hipEventRecord(ev[0], s);
-  hipLaunchKernelGGL((k_scan_lists<M, G, R, J, PF>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+  hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+#ifdef SCAN_TWICE  // diagnostic build only: re-scan with every query's tau already tight
+  (void)hipMemsetAsync(pl.hdr + 2, 0, sizeof(int32_t), s);
+  hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+#endif
   if (ev) (void)hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
@@ -1710,3 +1743,11 @@ void launch_merge_topk(int S, int64_t n, int k, const float* Din, const int64_t*
 }
 
 }  // namespace chivf
+
+#ifdef DIAG_STAMPS
+extern "C" int ivfpq_diag_stamps(void* out, size_t bytes) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(chivf::g_diag), bytes) != hipSuccess) return -1;
+  static uint64_t zeros[chivf::kDiagWG * chivf::kDiagItems * chivf::kDiagSlots];
+  return hipMemcpyToSymbol(HIP_SYMBOL(chivf::g_diag), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
