@@ -361,6 +361,30 @@ __device__ __forceinline__ void wave_kway(float (&d)[KL], int64_t (&id)[KL], int
   }
 }
 
+// k-th smallest (k <= 64) of the wave's 64 values: ascending bitonic sort of
+// the values alone (no ids), then a readlane.
+__device__ __forceinline__ float wave_kth_smallest(float m, int k, int lane) {
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      float o;
+      switch (j) {
+        case 1: o = xor_f<1>(m); break;
+        case 2: o = xor_f<2>(m); break;
+        case 4: o = xor_f<4>(m); break;
+        case 8: o = xor_f<8>(m); break;
+        case 16: o = xor_f<16>(m); break;
+        default: o = xor_f<32>(m); break;
+      }
+      const bool up = (lane & kk) == 0 || kk == 64;
+      const bool lower = (lane & j) == 0;
+      m = (lower == up) ? fminf(m, o) : fmaxf(m, o);
+    }
+  }
+  return readlane_f(m, k - 1);
+}
+
 // Threshold pre-filter for the same selection (lanes' 16 entries unsorted):
 // T = the k-th smallest of the 64 lane minima bounds the k-th smallest entry
 // (those k minima are k distinct entries <= T), so every entry of the top-k by
@@ -912,11 +936,15 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
   }
 }
 
-// Work items from the per-list counts.  Every workgroup re-derives the item
-// offsets of the lists before its own 1024 (a reduction over the counts), scans
-// its own lists' item counts in LDS, and writes the records of its items, one
-// item per thread.  Items of kind 0 occupy [0, N0), kind 1 [N0, N0 + N1).
+// Work items from the per-list counts.  Items of kind 0 occupy [0, N0), kind 1
+// [N0, N0 + N1), each in list order.  Small shard ranges (nloc <=
+// kPlanSmall): every workgroup builds the whole per-list item prefix in LDS
+// and writes the records of its 1024 items, one per thread (the grid covers
+// the item-count bound).  Large ranges: every workgroup takes 1024 lists,
+// derives the items before them by a reduction over the counts, and writes its
+// lists' items.
 constexpr int PLAN_T = 1024;
+constexpr int kPlanSmall = 4096;
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
@@ -927,12 +955,109 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
   return v;
 }
 
-__global__ __launch_bounds__(PLAN_T) void k_plan_items(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
-                                                       int nloc, int G) {
-  __shared__ int red[4][PLAN_T / 64];
-  __shared__ int ex0[PLAN_T + 1], ex1[PLAN_T + 1];
+// exclusive scan of (a, b) over the 1024 threads of the block; returns the block totals
+__device__ __forceinline__ void block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, int* ws /* [2][16] */) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NW = PLAN_T / 64;
+  const int ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane);
+  __syncthreads();  // ws may still be read by a previous call
+  if (lane == 63) {
+    ws[wave] = ia;
+    ws[16 + wave] = ib;
+  }
+  __syncthreads();
+  int pa = 0, pb = 0;
+  ta = 0;
+  tb = 0;
+  for (int w = 0; w < PLAN_T / 64; w++) {
+    const int va = ws[w], vb = ws[16 + w];
+    if (w < wave) {
+      pa += va;
+      pb += vb;
+    }
+    ta += va;
+    tb += vb;
+  }
+  ea = pa + ia - a;
+  eb = pb + ib - b;
+}
+
+__device__ __forceinline__ void write_item(const ListPlan& pl, const int64_t* __restrict__ list_off, int lo, int nloc,
+                                           int G, int rec, int jj, int kind, int t) {
+  const int c = min(pl.cnt[kind * nloc + jj], pl.cap);
+  const int cnt = min(G, c - t * G);
+  const int64_t l = lo + jj;
+  const int64_t beg = list_off[l];
+  int r[16];
+  r[0] = (int)l;
+  r[1] = cnt;
+  r[2] = (int)(list_off[l + 1] - beg);
+  r[3] = (int)(uint32_t)(uint64_t)beg;
+  r[4] = (int)(uint32_t)((uint64_t)beg >> 32);
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    int2 v = make_int2(0, 0);
+    if (g < cnt) v = pl.bucket[((int64_t)jj * 2 + kind) * pl.cap + t * G + g];
+    r[5 + g] = v.x;
+    r[9 + g] = v.y;
+  }
+  r[13] = kind;
+  r[14] = 0;
+  r[15] = 0;
+  int4* rp = reinterpret_cast<int4*>(pl.recs + (int64_t)rec * 16);
+  rp[0] = make_int4(r[0], r[1], r[2], r[3]);
+  rp[1] = make_int4(r[4], r[5], r[6], r[7]);
+  rp[2] = make_int4(r[8], r[9], r[10], r[11]);
+  rp[3] = make_int4(r[12], r[13], r[14], r[15]);
+}
+
+__global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
+                                                             int nloc, int G) {
+  __shared__ int ex[2][kPlanSmall + 1];
+  __shared__ int ws[32];
+  const int tid = threadIdx.x;
+  // per-list exclusive prefix of the item counts, both kinds, in chunks of 1024 lists
+  int ca = 0, cb = 0;
+  for (int j0 = 0; j0 < nloc; j0 += PLAN_T) {
+    const int j = j0 + tid;
+    const int a = j < nloc ? (min(pl.cnt[j], pl.cap) + G - 1) / G : 0;
+    const int b = j < nloc ? (min(pl.cnt[nloc + j], pl.cap) + G - 1) / G : 0;
+    int ea, eb, ta, tb;
+    block_scan2(a, b, ea, eb, ta, tb, ws);
+    if (j < nloc) {
+      ex[0][j] = ca + ea;
+      ex[1][j] = cb + eb;
+    }
+    ca += ta;
+    cb += tb;
+  }
+  if (tid == 0) {
+    ex[0][nloc] = ca;
+    ex[1][nloc] = cb;
+  }
+  const int T0 = ca, N = ca + cb;
+  if (blockIdx.x == 0 && tid < 16) pl.hdr[tid] = tid == 0 ? N : tid == 1 ? T0 : 0;
+  __syncthreads();
+  const int e = blockIdx.x * PLAN_T + tid;
+  if (e >= N) return;
+  const int kind = e < T0 ? 0 : 1;
+  const int ek = kind ? e - T0 : e;
+  const int* exk = ex[kind];
+  int lo_i = 0, hi_i = nloc;  // largest j with exk[j] <= ek
+  while (hi_i - lo_i > 1) {
+    const int mid = (lo_i + hi_i) >> 1;
+    if (exk[mid] <= ek)
+      lo_i = mid;
+    else
+      hi_i = mid;
+  }
+  write_item(pl, list_off, lo, nloc, G, e, lo_i, kind, ek - exk[lo_i]);
+}
+
+__global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
+                                                           int nloc, int G) {
+  __shared__ int ex0[PLAN_T + 1], ex1[PLAN_T + 1];
+  __shared__ int ws[32];
+  const int tid = threadIdx.x;
   const int my0 = blockIdx.x * PLAN_T;
   int t0 = 0, t1 = 0, p0 = 0, p1 = 0;
   for (int j = tid; j < nloc; j += PLAN_T) {
@@ -944,43 +1069,19 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items(ListPlan pl, const int64_
       p1 += b;
     }
   }
-  t0 = wave_incl_scan(t0, lane);
-  t1 = wave_incl_scan(t1, lane);
-  p0 = wave_incl_scan(p0, lane);
-  p1 = wave_incl_scan(p1, lane);
-  if (lane == 63) {
-    red[0][wave] = t0;
-    red[1][wave] = t1;
-    red[2][wave] = p0;
-    red[3][wave] = p1;
-  }
-  // own lists: item counts and their exclusive scan
+  int ea, eb, T0, T1, P0, P1;
+  block_scan2(t0, t1, ea, eb, T0, T1, ws);
+  block_scan2(p0, p1, ea, eb, P0, P1, ws);
   const int j = my0 + tid;
   const int a = j < nloc ? (min(pl.cnt[j], pl.cap) + G - 1) / G : 0;
   const int b = j < nloc ? (min(pl.cnt[nloc + j], pl.cap) + G - 1) / G : 0;
-  const int ia = wave_incl_scan(a, lane), ib = wave_incl_scan(b, lane);
-  __shared__ int wsa[NW], wsb[NW];
-  if (lane == 63) {
-    wsa[wave] = ia;
-    wsb[wave] = ib;
-  }
-  __syncthreads();
-  int T0 = 0, T1 = 0, P0 = 0, P1 = 0, ba = 0, bb = 0;
-  for (int w = 0; w < NW; w++) {
-    T0 += red[0][w];
-    T1 += red[1][w];
-    P0 += red[2][w];
-    P1 += red[3][w];
-    if (w < wave) {
-      ba += wsa[w];
-      bb += wsb[w];
-    }
-  }
-  ex0[tid + 1] = ba + ia;
-  ex1[tid + 1] = bb + ib;
+  int sa, sb;
+  block_scan2(a, b, ea, eb, sa, sb, ws);
+  ex0[tid] = ea;
+  ex1[tid] = eb;
   if (tid == 0) {
-    ex0[0] = 0;
-    ex1[0] = 0;
+    ex0[PLAN_T] = sa;
+    ex1[PLAN_T] = sb;
   }
   if (blockIdx.x == 0 && tid < 16) pl.hdr[tid] = tid == 0 ? T0 + T1 : tid == 1 ? T0 : 0;
   __syncthreads();
@@ -988,47 +1089,16 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items(ListPlan pl, const int64_
   for (int e = tid; e < own0 + own1; e += PLAN_T) {
     const int kind = e < own0 ? 0 : 1;
     const int ek = kind ? e - own0 : e;
-    const int* ex = kind ? ex1 : ex0;
-    int lo_i = 0, hi_i = PLAN_T;  // largest jl with ex[jl] <= ek
+    const int* exk = kind ? ex1 : ex0;
+    int lo_i = 0, hi_i = PLAN_T;  // largest jl with exk[jl] <= ek
     while (hi_i - lo_i > 1) {
       const int mid = (lo_i + hi_i) >> 1;
-      if (ex[mid] <= ek)
+      if (exk[mid] <= ek)
         lo_i = mid;
       else
         hi_i = mid;
     }
-    const int jl = lo_i;
-    const int t = ek - ex[jl];
-    const int jj = my0 + jl;
-    const int c = min(pl.cnt[kind * nloc + jj], pl.cap);
-    const int cnt = min(G, c - t * G);
-    const int64_t l = lo + jj;
-    const int64_t beg = list_off[l];
-    const int rec = kind ? T0 + P1 + ek : P0 + ek;
-    int r[16];
-    r[0] = (int)l;
-    r[1] = cnt;
-    r[2] = (int)(list_off[l + 1] - beg);
-    r[3] = (int)(uint32_t)(uint64_t)beg;
-    r[4] = (int)(uint32_t)((uint64_t)beg >> 32);
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-      int2 v = make_int2(0, 0);
-      if (g < cnt) {
-        const int s = t * G + g;
-        v = pl.bucket[((int64_t)jj * 2 + kind) * pl.cap + s];
-      }
-      r[5 + g] = v.x;
-      r[9 + g] = v.y;
-    }
-    r[13] = kind;
-    r[14] = 0;
-    r[15] = 0;
-    int4* rp = reinterpret_cast<int4*>(pl.recs + (int64_t)rec * 16);
-    rp[0] = make_int4(r[0], r[1], r[2], r[3]);
-    rp[1] = make_int4(r[4], r[5], r[6], r[7]);
-    rp[2] = make_int4(r[8], r[9], r[10], r[11]);
-    rp[3] = make_int4(r[12], r[13], r[14], r[15]);
+    write_item(pl, list_off, lo, nloc, G, kind ? T0 + P1 + ek : P0 + ek, my0 + lo_i, kind, ek - exk[lo_i]);
   }
 }
 
@@ -1136,6 +1206,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   __shared__ float qd[4][QCAP];
   __shared__ int32_t qi[4][QCAP];  // (position in the list << 2) | g
   __shared__ int s_next;
+  __shared__ int32_t s_wb[G];  // the item's per-query bounds found by its waves (ordered ints)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1148,21 +1219,23 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   const int n_items = pl.hdr[0];
   const uint64_t lanemask_lt = (1ull << lane) - 1;
 
+  // An item's 64-B record: lanes 0..15 load its 16 words (vector loads, kept in
+  // flight while the previous item is scanned), unpacked with readlane.
   Item<G> it;
-  auto load_item = [&](int idx) __attribute__((always_inline)) {
-    const int4* rp = reinterpret_cast<const int4*>(pl.recs + (int64_t)__builtin_amdgcn_readfirstlane(idx) * 16);
-    const int4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
-    it.l = r0.x;
-    it.cnt = r0.y;
-    it.n = r0.z;
-    it.beg = (int64_t)(((uint64_t)(uint32_t)r1.x << 32) | (uint32_t)r0.w);
-    it.kind = r3.y;
-    const int pr[4] = {r1.y, r1.z, r1.w, r2.x};
-    const int db[4] = {r2.y, r2.z, r2.w, r3.x};
+  auto fetch_rec = [&](int idx) __attribute__((always_inline)) -> int {
+    return pl.recs[(int64_t)idx * 16 + (lane & 15)];
+  };
+  auto unpack = [&](int rv) __attribute__((always_inline)) {
+    it.l = __builtin_amdgcn_readlane(rv, 0);
+    it.cnt = __builtin_amdgcn_readlane(rv, 1);
+    it.n = __builtin_amdgcn_readlane(rv, 2);
+    it.beg = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane(rv, 3));
+    it.kind = __builtin_amdgcn_readlane(rv, 13);
 #pragma unroll
     for (int g = 0; g < G; g++) {
-      it.pair[g] = pr[g];
-      it.d0[g] = __int_as_float(db[g]);
+      it.pair[g] = __builtin_amdgcn_readlane(rv, 5 + g);
+      it.d0[g] = __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g));
     }
   };
 
@@ -1172,14 +1245,20 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   }
   __syncthreads();
   int cur = s_next;
-  if (cur >= 0) load_item(cur);
+  if (cur >= 0) unpack(fetch_rec(cur));
   int it_no = 0;
   (void)it_no;
   while (cur >= 0) {
     __syncthreads();  // (A) every wave is done with the LUT of the previous item, and has read s_next
     DIAG(0, __builtin_amdgcn_s_memtime());
-    int tnext = 0;
-    if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);  // the next item; consumed after the LUT build
+    // the next item, consumed after the LUT build (tnext is left undefined in the
+    // other lanes: no merge copy that would wait for the atomic right here)
+    int tnext;
+    if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);
+    // the queries' running k-th keys, read with the LUT rows (a stale value is only a looser bound)
+    int tq[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) tq[g] = pl.tauq[(g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe];
     // the item's first JB x 256 codes, issued with the LUT rows (one round trip for both)
     const int n = it.n;
     const uint8_t* lc = a.codes + it.beg * M;
@@ -1187,46 +1266,75 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
     for (int j = 0; j < JB; j++) {
       const int i = j * 256 + wave * 64 + lane;
+#ifdef DIAG_NOCODES
+      for (int v = 0; v < M / 4; v++) cw[j].w[v] = (uint32_t)(i * 0x9E3779B1u + v);
+#else
       cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
+#endif
     }
-    {  // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
-      const float4* T1l = reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
+    {  // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0.
+      // Software-pipelined in groups of U float4 rows per thread: the loads of
+      // group u + 1 are in flight while group u is combined and stored.
       const float4* T3q[G];
 #pragma unroll
       for (int g = 0; g < G; g++)
         T3q[g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)((g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe) * LUTN);
-#pragma unroll 4
-      for (int e = 0; e < NV; e++) {
-        const int v = e * 256 + tid;
-        const float4 t1 = ip ? make_float4(0.f, 0.f, 0.f, 0.f) : T1l[v];
-        float4 t3[G];
+      // IP has no T1: read (and ignore) a T3 row instead, so that every load is unconditional
+      const float4* T1l = ip ? T3q[0] : reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
+      constexpr int U = NV < 4 ? NV : 4;
+      constexpr int NG = NV / U;
+      static_assert(NV % U == 0, "LUT rows per thread");
+      float4 b1[2][U], b3[2][U][G];
+      auto fetch = [&](int u, int buf) __attribute__((always_inline)) {
 #pragma unroll
-        for (int g = 0; g < G; g++) t3[g] = T3q[g][v];
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          V o;
+        for (int e = 0; e < U; e++) {
+          const int v = (u * U + e) * 256 + tid;
+          b1[buf][e] = T1l[v];
 #pragma unroll
           for (int g = 0; g < G; g++) {
-            const float x3 = comp(t3[g], c);
-            const float lv = ip ? -x3 : comp(t1, c) + (-2.0f * x3);
-            setc(o, g, g < it.cnt ? lv : 0.f);
+#ifdef DIAG_NOT3
+            b3[buf][e][g] = make_float4(g, v, 0, 1);
+#else
+            b3[buf][e][g] = T3q[g][v];
+#endif
           }
-          lut[4 * v + c] = o;
+        }
+      };
+      fetch(0, 0);
+#pragma unroll
+      for (int u = 0; u < NG; u++) {
+        if (u + 1 < NG) fetch(u + 1, (u + 1) & 1);
+#pragma unroll
+        for (int e = 0; e < U; e++) {
+          const int v = (u * U + e) * 256 + tid;
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            V o;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              const float x3 = comp(b3[u & 1][e][g], c);
+              const float lv = ip ? -x3 : comp(b1[u & 1][e], c) + (-2.0f * x3);
+              setc(o, g, g < it.cnt ? lv : 0.f);
+            }
+            lut[4 * v + c] = o;
+          }
         }
       }
     }
     if (tid == 0) s_next = tnext < n_items ? tnext : -1;
-    __syncthreads();  // (B) the LUT and s_next are visible
+    if (tid < G) s_wb[tid] = f2ord(kInf);
+    __syncthreads();  // (B) the LUT, s_next and s_wb are visible
     DIAG(1, __builtin_amdgcn_s_memtime());
     const Item<G> ci = it;
     const int nxt = s_next;
+    const int nrec = fetch_rec(nxt >= 0 ? nxt : cur);  // the next record, in flight during the scan
     int64_t qix[G];
     float bound[G];
     bool loose = false;  // some query of the item has no bound yet
 #pragma unroll
     for (int g = 0; g < G; g++) {
       qix[g] = (g < ci.cnt ? ci.pair[g] : 0) / a.nprobe;
-      bound[g] = g < ci.cnt ? ord2f(pl.tauq[qix[g]]) : -kInf;
+      bound[g] = g < ci.cnt ? ord2f(tq[g]) : -kInf;
       loose = loose || bound[g] == kInf;
     }
 
@@ -1236,11 +1344,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     int qn = 0;  // this wave's queue fill (wave-uniform)
 #ifdef DIAG_STAMPS
     int npush = 0;
+    uint64_t tdrain = 0;
 #ifdef DIAG_FINE
     asm volatile("" ::"v"(bound[0]), "v"(bound[G - 1]));
     DIAG(6, __builtin_amdgcn_s_memtime());
-#else
-    DIAG(7, (uint32_t)f2ord(bound[0]));
 #endif
 #endif
 
@@ -1274,14 +1381,18 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
       for (int g = 0; g < G; g++) {
         loose = loose || bound[g] == kInf;
-        if (g < ci.cnt && tk[g].td < kInf && lane == 0) atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td));
+        if (g < ci.cnt && tk[g].td < kInf && lane == 0) {
+          atomicMin(&s_wb[g], f2ord(tk[g].td));
+          atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td));
+        }
       }
     };
 
-    // Chunks of 64 codes per wave (256 per workgroup), JB of them held in
-    // registers.  The chunks run as a straight sequence of guarded blocks
-    // (compile-time register indices, no selection network) that stops where
-    // the queue needs draining; one drain site serves every stop.
+    // Chunks of 64 codes per wave (256 per workgroup), JB of them per super-batch:
+    // all of a super-batch's keys are gathered first (held in registers), then
+    // admitted chunk by chunk.  A straight sequence of guarded blocks
+    // (compile-time register indices, no selection network) stops where the
+    // queue needs draining; one drain site serves every stop.
     for (int sb = 0; sb < n; sb += 256 * JB) {
       if (sb > 0) {
 #pragma unroll
@@ -1298,80 +1409,135 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       }
 #endif
       const bool last_sb = sb + 256 * JB >= n;
+      // G keys per code: dis0 + sum_m LUT[m][code_m], sequential in m (the
+      // oracle's order); two chunks at a time, their 2 x M LDS gathers
+      // interleaved m-outer for latency hiding
+      float dis[JB][G];
+      static_assert(JB % 2 == 0, "chunks are gathered in pairs");
+#pragma unroll
+      for (int jd = 0; jd < JB / 2; jd++) {
+        if (2 * jd < tn) {  // wave-uniform
+          // opaque copies of the words: keep the LUT addresses of all chunks from
+          // being computed up front
+          CodeWords<M> cc[2] = {cw[2 * jd], cw[2 * jd + 1]};
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(cc[h].w[v]));
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int g = 0; g < G; g++) dis[2 * jd + h][g] = ci.d0[g];
+#pragma unroll
+          for (int m = 0; m < M; m++) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+#ifdef DIAG_NOGATHER
+              V v;
+              for (int g = 0; g < G; g++) setc(v, g, __int_as_float(cc[h].byte(m)));
+#else
+              const V v = lut[m * 256 + cc[h].byte(m)];
+#endif
+#pragma unroll
+              for (int g = 0; g < G; g++) dis[2 * jd + h][g] = dis[2 * jd + h][g] + comp(v, g);
+            }
+          }
+        }
+      }
+#ifdef DIAG_NOADMIT
+      asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1]));
+      continue;
+#endif
+      if constexpr (R == 1) {
+        // A query without a bound gets one from this super-batch: the k-th
+        // smallest of the 64 lane minima bounds the final k-th key (those minima
+        // are k distinct codes), so only about k codes per wave are admitted
+        // instead of every code until the wave's own top-k has filled.  The bound
+        // is shared with the other waves (LDS) and workgroups (tau_q).
+        if (loose) {
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (bound[g] != kInf) continue;  // wave-uniform
+            float mn = kInf;
+#pragma unroll
+            for (int j = 0; j < JB; j++)
+              if (j < tn && sb + j * 256 + wave * 64 + lane < n) mn = fminf(mn, dis[j][g]);
+            const float T = wave_kth_smallest(mn, k, lane);
+            if (T < kInf && lane == 0) {
+              atomicMin(&s_wb[g], f2ord(T));
+              atomicMin(&pl.tauq[qix[g]], f2ord(T));
+            }
+          }
+        }
+      }
+      loose = false;
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (g < ci.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));
+        loose = loose || bound[g] == kInf;
+      }
       int t = 0;
       while (true) {
         int stop = tn;       // first chunk not yet admitted
         bool want = false;   // drain requested
-        // one chunk: G keys per code (dis0 + sum_m LUT[m][code_m], sequential in
-        // m: the oracle's order), then admission into the queue
-        auto chunk = [&](int j, const CodeWords<M>& c0) __attribute__((always_inline)) -> bool {
-          // opaque copy of the words: keeps the LUT addresses of all JB chunks from
-          // being hoisted out of the restart loop (128 live VGPRs at JB = 8)
-          CodeWords<M> c = c0;
-#pragma unroll
-          for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(c.w[v]));
-          const int i = sb + j * 256 + wave * 64 + lane;
-          float dis[G];
-#pragma unroll
-          for (int g = 0; g < G; g++) dis[g] = ci.d0[g];
-#pragma unroll
-          for (int m = 0; m < M; m++) {
-#ifdef DIAG_NOGATHER
-            V v;
-            for (int g = 0; g < G; g++) setc(v, g, __int_as_float(c.byte(m)));
-#else
-            const V v = lut[m * 256 + c.byte(m)];
-#endif
-#pragma unroll
-            for (int g = 0; g < G; g++) dis[g] = dis[g] + comp(v, g);
-          }
-          const bool valid = i < n;
-          uint64_t mk[G];
-          int tj = 0;
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            mk[g] = __builtin_amdgcn_ballot_w64(valid && dis[g] <= bound[g]);
-            tj += __popcll(mk[g]);
-          }
-          if (tj == 0) return false;
-          if (qn + tj > QCAP) {  // no room: drain first, then redo this chunk
-            stop = j;
-            want = true;
-            return true;
-          }
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            if ((mk[g] >> lane) & 1) {
-              const int sl = qn + __popcll(mk[g] & lanemask_lt);
-              qd[wave][sl] = dis[g];
-              qi[wave][sl] = (i << 2) | g;
-            }
-            qn += __popcll(mk[g]);
-          }
-#ifdef DIAG_STAMPS
-          npush += tj;
-#endif
-          if (loose) {  // a query of the item has no bound yet: get one now
-            stop = j + 1;
-            want = true;
-            return true;
-          }
-          return false;
-        };
         bool go = true;
 #pragma unroll
         for (int j = 0; j < JB; j++) {
-          if (go && j >= t && j < tn) {  // wave-uniform guards: a straight sequence of chunks
-            if (chunk(j, cw[j])) go = false;
+          if (go && j >= t && j < tn) {  // wave-uniform
+            const int i = sb + j * 256 + wave * 64 + lane;
+            const bool valid = i < n;
+            uint64_t mk[G];
+            int tj = 0;
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              mk[g] = __builtin_amdgcn_ballot_w64(valid && dis[j][g] <= bound[g]);
+              tj += __popcll(mk[g]);
+            }
+            if (tj > 0) {
+              if (qn + tj > QCAP) {  // no room: drain first, then redo this chunk
+                stop = j;
+                want = true;
+                go = false;
+              } else {
+#pragma unroll
+                for (int g = 0; g < G; g++) {
+                  if ((mk[g] >> lane) & 1) {
+                    const int sl = qn + __popcll(mk[g] & lanemask_lt);
+                    qd[wave][sl] = dis[j][g];
+                    qi[wave][sl] = (i << 2) | g;
+                  }
+                  qn += __popcll(mk[g]);
+                }
+#ifdef DIAG_STAMPS
+                npush += tj;
+#endif
+                if (loose) {  // a query of the item has no bound yet: get one now
+                  stop = j + 1;
+                  want = true;
+                  go = false;
+                }
+              }
+            }
           }
         }
-        if (want || (stop >= tn && last_sb && qn > 0)) drain();
+        if (want || (stop >= tn && last_sb && qn > 0)) {
+#ifdef DIAG_STAMPS
+          const uint64_t td0 = __builtin_amdgcn_s_memtime();
+          drain();
+          tdrain += __builtin_amdgcn_s_memtime() - td0;
+#else
+          drain();
+#endif
+        }
         if (stop >= tn) break;
         t = stop;
       }
     }
     DIAG(2, __builtin_amdgcn_s_memtime());
 #ifdef DIAG_STAMPS
+#ifndef DIAG_FINE
+    DIAG(7, tdrain);
+#endif
     DIAG(4, n);
     DIAG(5, ci.cnt | (ci.kind << 8));
 #ifndef DIAG_FINE
@@ -1379,6 +1545,8 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #endif
 #endif
 
+    // the next item's fields (before the stores below, which a later wait would also cover)
+    if (nxt >= 0) unpack(nrec);
     // each wave writes its own sorted partial list per pair (merged by k_merge_probes)
 #pragma unroll
     for (int g = 0; g < G; g++) {
@@ -1394,7 +1562,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         }
       }
     }
-    if (nxt >= 0) load_item(nxt);
     DIAG(3, __builtin_amdgcn_s_memtime());
     it_no++;
     cur = nxt;
@@ -1667,8 +1834,12 @@ void launch_plan_count(const int64_t* lists, const float* Dq, const float* x, co
 
 void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int hi, int G, hipStream_t s) {
   const int nloc = hi - lo;
-  hipLaunchKernelGGL(k_plan_items, dim3(std::max(1u, nblocks(nloc, PLAN_T))), dim3(PLAN_T), 0, s, pl, list_off, lo,
-                     nloc, G);
+  if (nloc <= kPlanSmall)
+    hipLaunchKernelGGL(k_plan_items_small, dim3(std::max(1u, nblocks(pl.max_items, PLAN_T))), dim3(PLAN_T), 0, s, pl,
+                       list_off, lo, nloc, G);
+  else
+    hipLaunchKernelGGL(k_plan_items_big, dim3(std::max(1u, nblocks(nloc, PLAN_T))), dim3(PLAN_T), 0, s, pl, list_off,
+                       lo, nloc, G);
 }
 
 bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 || M == 64; }
@@ -1702,7 +1873,7 @@ int scan_lists_grid() {
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 8) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 8) ? 2 : 1;
-  constexpr int JB = M <= 16 ? 8 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs)
+  constexpr int JB = M <= 16 ? 8 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs), even
   if (ev) (void)hipEventRecord(ev[0], s);
   hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
 #ifdef SCAN_TWICE  // diagnostic build only: re-scan with every query's tau already tight

@@ -9,7 +9,7 @@ for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   O=$R/chameleon-rag-acceleration_amd/lib/var/$name
   mkdir -p "$O"
-  /opt/rocm/bin/hipcc $F $defs -c -o "$O/k.o" "$C/ivfpq_kernels.hip" &
+  /opt/rocm/bin/hipcc $F -mllvm -amdgpu-atomic-optimizer-strategy=None $defs -c -o "$O/k.o" "$C/ivfpq_kernels.hip" &
   /opt/rocm/bin/hipcc $F $defs -x hip -c -o "$O/i.o" "$C/ivfpq_index.cpp" &
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libivfpq.so" "$O/k.o" "$O/i.o"

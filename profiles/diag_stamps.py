@@ -1,5 +1,10 @@
 """Per-item phase breakdown of k_scan_lists from a DIAG_STAMPS build.
 
+Slots per (workgroup, iteration): 0 scanners start, 1 builders done (the
+next item's LUT), 2 scanners' gathers done, 3 partial writes done, 4 codes,
+5 pairs | kind << 8, 6 admitted candidates (scanner wave 0).  "build" is the
+builders' time for the NEXT item measured from this iteration's start.
+
 Usage (on the GPU box):
   bash profiles/build_variants.sh diag:"-DDIAG_STAMPS=1"     # here, before gpurun
   IVFPQ_LIB=chameleon-rag-acceleration_amd/lib/var/diag/libivfpq.so python3 profiles/diag_stamps.py
@@ -57,11 +62,12 @@ def main():
         if not sel.any():
             continue
         print(f"-- {kname}: codes/item {n[sel].mean():.0f}, pairs/item {cnt[sel].mean():.2f}, "
-              f"admitted (wave 0, all g) per item {push[sel].mean():.1f}, tau=inf at start "
-              f"{(tau[sel] == 0x7F800000).mean():.2f}")
+              f"admitted (wave 0, all g) per item {push[sel].mean():.1f}")
         for name, v in (("build", (t1 - t0)[sel]), ("scan", (t2 - t1)[sel]), ("write", (t3 - t2)[sel])):
             print(f"   {name:6s} cycles mean {v.mean():8.0f} p50 {np.median(v):8.0f} p90 {np.percentile(v, 90):8.0f}")
         sc = (t2 - t1)[sel]
+        if not os.environ.get("FINE"):
+            print(f"   drain cycles (wave 0) mean {tau[sel].mean():.0f} p50 {np.median(tau[sel]):.0f}")
         print(f"   scan cycles per code-pair {sc.sum() / (n[sel] * cnt[sel]).sum():.2f}, per code {sc.sum() / n[sel].sum():.2f}")
     first = np.where(valid, t0, np.iinfo(np.int64).max).min(1)
     last = np.where(valid, t3, 0).max(1)
