@@ -409,24 +409,20 @@ struct ivfpq_index {
   bool ip() const { return metric == IVFPQ_METRIC_INNER_PRODUCT; }
 
   // Coarse quantizer for c queries at x: the nprobe best lists and the
-  // quantizer's values (L2 distances / IP similarities).  With `plan` (and
-  // nprobe <= 64, nlist within the fused kernel's LDS) the fused kernel also
-  // plans the batch and builds T3 and true is returned; otherwise the caller
-  // plans with launch_plan_count and builds T3 with launch_ip_table.
+  // quantizer's values (L2 distances / IP similarities), from the key matrix
+  // built on the matrix cores (with T3out, the same launch builds T3).  With
+  // `plan` and nprobe <= 64 the selection also plans the batch and true is
+  // returned; otherwise the caller plans with launch_plan_count.
   bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
-                     const ListPlan* plan = nullptr) {
-    if (coarse_fused_ok(nlist, np, d)) {
-      const bool planned = plan && np <= 64;
-      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, ip(),
-                          planned ? plan : nullptr, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>(),
-                          planned ? w_T3.as<float>() : nullptr, d_cb.as<float>(), M);
-      return planned;
-    }
-    w_xn.ensure(sizeof(float) * c);
+                     const ListPlan* plan = nullptr, float* T3out = nullptr) {
     w_dist.ensure(sizeof(float) * c * nlist);
-    if (!ip()) launch_row_norms(x, c, d, w_xn.as<float>(), s);
-    launch_l2_dist(x, w_xn.as<float>(), c, d_cent.as<float>(), d_cnorm.as<float>(), nlist, d, w_dist.as<float>(), s,
-                   ip());
+    launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, w_dist.as<float>(), s, ip(), T3out,
+                       d_cb.as<float>(), M);
+    if (np <= 64) {
+      launch_coarse_select(w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
+                           list_hi, x, d_cent.as<float>(), d);
+      return plan != nullptr;
+    }
     launch_select_rows(w_dist.as<float>(), c, nlist, np, dis, lists, s, ip());
     return false;
   }
@@ -460,14 +456,14 @@ struct ivfpq_index {
         launch_plan_count(lists, (Dq && !ip()) ? Dq + q0 * np : nullptr, xq, d_cent.as<float>(), c, d, np,
                           d_off.as<int64_t>(), list_lo, list_hi, ip(), true, k, plan, s);
       } else {
-        planned = coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s, &plan);
+        planned = coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s, &plan, w_T3.as<float>());
         lists = w_lists.as<int64_t>();
         if (!planned)
           launch_plan_count(lists, ip() ? nullptr : w_dis0.as<float>(), xq, d_cent.as<float>(), c, d, np,
                             d_off.as<int64_t>(), list_lo, list_hi, ip(), false, k, plan, s);
       }
       mark_end(tm, s);
-      if (!planned) {
+      if (preassigned) {  // T3 (the coarse launch builds it otherwise)
         const int tt = mark_begin(ST_TABLES, s);
         launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
         mark_end(tt, s);

@@ -32,22 +32,20 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
 
 struct ListPlan;
 
-// Fused coarse quantizer (one launch): per query the keys to all centroids
-// (centT = centroids transposed [d][ldc], cn = |c|^2) and the nprobe smallest
-// (key, list) pairs; out_dis receives the quantizer's distances (L2) or
-// similarities (IP).  Same arithmetic as launch_l2_dist + launch_select_rows.
-// Requires nprobe <= 64 and (for LDS) nlist <= kCoarseFusedMax.
-// With `plan`, the epilogue also does the list-major planning of the batch
-// (first usable probe, tau reset, per-list pair counts, bucket entries with the
-// scan's dis0: L2 the coarse distance, IP -<x, c_l> in Faiss tree order over d)
-// and builds T3 [nq][M][256] (Faiss tree order) into T3out.
-constexpr int kCoarseFusedMax = 8192;
-bool coarse_fused_ok(int nlist, int nprobe, int d);
-void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, bool ip,
-                         const ListPlan* plan = nullptr, const int64_t* list_off = nullptr, int lo = 0, int hi = 0,
-                         const float* cent = nullptr, float* T3out = nullptr, const float* codebook = nullptr,
-                         int M = 0);
+// Coarse quantizer keys on the matrix cores: keys[q][c] (launch_l2_dist's
+// arithmetic; centT = centroids transposed [d][(nlist + 3) & ~3], cn = |c|^2).
+// With T3out, the same launch builds T3 [nq][M][256] (Faiss tree order).
+void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
+                        float* keys, hipStream_t s, bool ip, float* T3out = nullptr, const float* cb = nullptr,
+                        int M = 0);
+// Per query the nprobe (<= 64) smallest (key, list) pairs of a key matrix;
+// out_dis receives the quantizer's distances (L2) or similarities (IP).  With
+// `plan`, the epilogue also plans the batch (first usable probe, tau reset,
+// per-list pair counts, bucket entries with the scan's dis0: L2 the coarse
+// distance, IP -<x, c_l> in Faiss tree order over d).
+void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, float* out_dis, int64_t* out_list,
+                          hipStream_t s, bool ip, const ListPlan* plan = nullptr, const int64_t* list_off = nullptr,
+                          int lo = 0, int hi = 0, const float* x = nullptr, const float* cent = nullptr, int d = 0);
 
 // T3[q][m][j] = <x_q[m], C_mj>  (Faiss AVX order)
 void launch_ip_table(const float* x, int64_t n, int d, const float* codebook, int M, int ksub, float* out,

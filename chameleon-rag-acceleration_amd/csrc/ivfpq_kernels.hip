@@ -112,7 +112,10 @@ __device__ __forceinline__ float shr1_f(float old, float v) {
   return __int_as_float(dpp_shr1_i(__float_as_int(old), __float_as_int(v)));
 }
 
-// lane ^ J exchange: DPP for J <= 8, ds_swizzle for 16, bpermute for 32
+// lane ^ J exchange, all on the VALU: DPP for J <= 8, the gfx950 row / half
+// swaps for 16 and 32 (v_permlane16_swap / v_permlane32_swap of v with itself:
+// the first result holds the partner's value in the odd rows / upper half, the
+// second in the even rows / lower half).
 template <int CTRL>
 __device__ __forceinline__ int dmov(int v) {
   return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
@@ -123,11 +126,21 @@ __device__ __forceinline__ int xor_i(int v) {
   else if constexpr (J == 2) return dmov<0x4E>(v);             // quad_perm [2,3,0,1]
   else if constexpr (J == 4) return dmov<0x1B>(dmov<0x141>(v));  // row_half_mirror, quad_perm [3,2,1,0]
   else if constexpr (J == 8) return dmov<0x128>(v);            // row_ror:8
-  else if constexpr (J == 16) return __builtin_amdgcn_ds_swizzle(v, 0x401F);  // swap 16
-  else return __shfl_xor(v, 32, 64);
+  else if constexpr (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((__lane_id() & 16) ? r[0] : r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((__lane_id() & 32) ? r[0] : r[1]);
+  }
 }
 template <int J>
 __device__ __forceinline__ float xor_f(float v) { return __int_as_float(xor_i<J>(__float_as_int(v))); }
+// v[63 - lane] on the VALU: row_mirror, then the half and row swaps (row r -> 3 - r)
+__device__ __forceinline__ int rev64_i(int v) { return xor_i<16>(xor_i<32>(dmov<0x140>(v))); }
+__device__ __forceinline__ float rev64_f(float v) { return __int_as_float(rev64_i(__float_as_int(v))); }
+// v[lane ^ 15] (reverse inside each row of 16)
+__device__ __forceinline__ int rev16_i(int v) { return dmov<0x140>(v); }
 
 // Candidate ids: int64 labels / global positions, or int32 positions inside one
 // list (the list scan): half the cross-lane traffic of the top-k network.
@@ -147,18 +160,18 @@ __device__ __forceinline__ int64_t id_shr1(int64_t old, int64_t v) {
 }
 template <int J>
 __device__ __forceinline__ int id_xor(int v) { return xor_i<J>(v); }
+__device__ __forceinline__ int id_rev64(int v) { return rev64_i(v); }
+__device__ __forceinline__ int64_t id_rev64(int64_t v) {
+  const uint64_t u = (uint64_t)v;
+  const uint32_t lo = (uint32_t)rev64_i((int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)rev64_i((int)(uint32_t)(u >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 template <int J>
 __device__ __forceinline__ int64_t id_xor(int64_t v) {
   const uint64_t u = (uint64_t)v;
   const uint32_t lo = (uint32_t)xor_i<J>((int)(uint32_t)u);
   const uint32_t hi = (uint32_t)xor_i<J>((int)(uint32_t)(u >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ int id_shfl(int v, int src) { return __shfl(v, src, 64); }
-__device__ __forceinline__ int64_t id_shfl(int64_t v, int src) {
-  const uint64_t u = (uint64_t)v;
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)u, src, 64);
-  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(u >> 32), src, 64);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 template <class T>
@@ -238,7 +251,7 @@ struct WaveTopK {
 // Merge up to 64 candidates (one per lane; (inf, sentinel) = none) into a
 // single-row top-k: bitonic sort of the candidates, then the classic
 // reverse-min + bitonic merge against the sorted row.  Exchanges at strides
-// <= 8 are DPP moves, 16 a ds_swizzle, 32 a bpermute.
+// are VALU lane moves (xor_i).
 template <int KK, int J, class T>
 __device__ __forceinline__ void bitonic_step(float& cd, T& ci, int lane) {
   const float od = xor_f<J>(cd);
@@ -269,14 +282,44 @@ __device__ __forceinline__ void bitonic_sort64(float& cd, T& ci, int lane) {
 template <class T>
 __device__ __forceinline__ void bulk_merge_row(WaveTopK<1, T>& tk, float cd, T ci, int lane) {
   bitonic_sort64<2>(cd, ci, lane);
-  const float rd = __shfl(cd, 63 - lane, 64);
-  const T ri = id_shfl(ci, 63 - lane);
+  const float rd = rev64_f(cd);
+  const T ri = id_rev64(ci);
   if (lexless(rd, ri, tk.d[0], tk.id[0])) {
     tk.d[0] = rd;
     tk.id[0] = ri;
   }
   // ascending bitonic merge: KK = 128 keeps every lane "up"
   bitonic_steps<128, 32>(tk.d[0], tk.id[0], lane);
+  tk.refresh_tau();
+}
+
+// Merge up to 16 candidates held in lanes 0..15 (others (inf, none)) into a
+// single-row top-k with k <= 16: a 16-lane bitonic sort (DPP moves only), the
+// reverse-min against lanes 0..15 of the row, a 16-lane bitonic merge.  Only
+// lanes 0..15 of the row are kept (the rest are reset to (inf, none)).
+template <class T>
+__device__ __forceinline__ void row16_merge(WaveTopK<1, T>& tk, float cd, T ci, int lane) {
+  bitonic_steps<2, 1>(cd, ci, lane);
+  bitonic_steps<4, 2>(cd, ci, lane);
+  bitonic_steps<8, 4>(cd, ci, lane);
+  bitonic_steps<128, 8>(cd, ci, lane);  // KK = 128: every row ascending
+  const float rd = __int_as_float(rev16_i(__float_as_int(cd)));
+  T ri;
+  if constexpr (sizeof(T) == 8) {
+    const uint64_t u = (uint64_t)ci;
+    ri = (T)(((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(u >> 32)) << 32) | (uint32_t)rev16_i((int)(uint32_t)u));
+  } else {
+    ri = (T)rev16_i((int)ci);
+  }
+  if (lexless(rd, ri, tk.d[0], tk.id[0])) {
+    tk.d[0] = rd;
+    tk.id[0] = ri;
+  }
+  bitonic_steps<128, 8>(tk.d[0], tk.id[0], lane);
+  if (lane >= 16) {
+    tk.d[0] = kInf;
+    tk.id[0] = id_none<T>();
+  }
   tk.refresh_tau();
 }
 
@@ -385,70 +428,6 @@ __device__ __forceinline__ float wave_kth_smallest(float m, int k, int lane) {
   return readlane_f(m, k - 1);
 }
 
-// Threshold pre-filter for the same selection (lanes' 16 entries unsorted):
-// T = the k-th smallest of the 64 lane minima bounds the k-th smallest entry
-// (those k minima are k distinct entries <= T), so every entry of the top-k by
-// (dist, id) -- ties at T included -- has dist <= T.  When at most 64 entries
-// pass, they are compacted through `scratch` (>= 128 words of this wave's LDS,
-// no longer needed) and one 64-lane bitonic sort emits the k smallest in lanes
-// 0..k-1, exactly as wave_kway does.  Returns false (nothing written) when more
-// than 64 pass; the caller then runs lane_sort + wave_kway.
-__device__ __forceinline__ bool wave_select_threshold(const float (&d)[16], const int64_t (&id)[16], int k, int lane,
-                                                      float* scratch, float& out_d, int64_t& out_id) {
-  float m = d[0];
-#pragma unroll
-  for (int u = 1; u < 16; u++) m = fminf(m, d[u]);
-  // ascending bitonic sort of the lane minima (values only)
-#pragma unroll
-  for (int kk = 2; kk <= 64; kk <<= 1) {
-#pragma unroll
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      float o;
-      switch (j) {
-        case 1: o = xor_f<1>(m); break;
-        case 2: o = xor_f<2>(m); break;
-        case 4: o = xor_f<4>(m); break;
-        case 8: o = xor_f<8>(m); break;
-        case 16: o = xor_f<16>(m); break;
-        default: o = xor_f<32>(m); break;
-      }
-      const bool up = (lane & kk) == 0 || kk == 64;
-      const bool lower = (lane & j) == 0;
-      m = (lower == up) ? fminf(m, o) : fmaxf(m, o);
-    }
-  }
-  const float T = readlane_f(m, k - 1);
-  int c = 0;
-#pragma unroll
-  for (int u = 0; u < 16; u++) c += d[u] <= T ? 1 : 0;
-  // inclusive wave prefix sum of the per-lane counts
-  int incl = c;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
-  }
-  const int total = __builtin_amdgcn_readlane(incl, 63);
-  if (total > 64) return false;
-  int pos = incl - c;
-  int32_t* sid = reinterpret_cast<int32_t*>(scratch + 64);
-#pragma unroll
-  for (int u = 0; u < 16; u++) {
-    if (d[u] <= T) {
-      scratch[pos] = d[u];
-      sid[pos] = (int32_t)id[u];  // list numbers (< 2^31)
-      pos++;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  float cd = lane < total ? scratch[lane] : kInf;
-  int64_t ci = lane < total ? (int64_t)sid[lane] : kSentinelId;
-  bitonic_sort64<2>(cd, ci, lane);
-  out_d = lane < k ? cd : kInf;
-  out_id = lane < k ? ci : kSentinelId;
-  return true;
-}
-
 // order-preserving int image of a float (signed int compare == float compare),
 // for atomicMin on keys that may be negative (IP keys, rounding-negative L2)
 __device__ __forceinline__ int f2ord(float f) {
@@ -542,224 +521,38 @@ __device__ __forceinline__ void plan_pair(const ListPlan& pl, int nloc, int64_t 
   if (s < pl.cap) pl.bucket[((int64_t)(l - lo) * 2 + kind) * pl.cap + s] = make_int2(pair, __float_as_int(dis0));
 }
 
-// ------------------------------------------------------- fused coarse probe
-// 4 queries per 256-thread workgroup.  Thread t owns centroids 4t..4t+3 of each
-// 1024-centroid block (float4 loads of the transposed centroids, coalesced) and
-// accumulates <x_q, c> as a k-ordered fmaf chain for the 4 queries (query
-// elements broadcast from LDS).  Keys land in LDS; wave w then selects
-// query w's nprobe smallest (same rule and arithmetic as k_l2_dist +
-// k_select_rows).
-constexpr int CQ = 4;
+#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS)  // diagnostic builds only (profiles/diag_*.py)
+constexpr int kDiagWG = 1024, kDiagItems = 64, kDiagSlots = 8;
+__device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
+#endif
+#ifdef DIAG_CSTAMPS  // k_coarse_fused phase stamps per (workgroup, wave)
+#define CDIAG(slot)                                                                                  \
+  do {                                                                                               \
+    if (lane == 0 && blockIdx.x < kDiagWG)                                                           \
+      g_diag[((size_t)blockIdx.x * kDiagItems + wave) * kDiagSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define SDIAG(slot)                                                                                  \
+  do {                                                                                               \
+    if (lane == 0 && blockIdx.x < kDiagWG)                                                           \
+      g_diag[((size_t)blockIdx.x * kDiagItems + 4 + wave) * kDiagSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define CDIAG(slot) \
+  do {              \
+  } while (0)
+#define SDIAG(slot) \
+  do {              \
+  } while (0)
+#endif
 
+// List-major planning request for the coarse selection's epilogue.
 struct CoarsePlan {
   ListPlan pl;
   int on = 0;                         // 0: no planning (nprobe > 64, or not requested)
   const int64_t* list_off = nullptr;
   int lo = 0, hi = 0;
   const float* cent = nullptr;        // [nlist][d] row-major (IP dis0)
-  float* T3out = nullptr;             // [nq][M][256] (null: no T3)
-  const float* cb = nullptr;
-  int M = 0;
 };
-
-template <int R>
-__global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
-                                                      const float* __restrict__ centT, const float* __restrict__ cn,
-                                                      int nlist, int nprobe, float* __restrict__ out_dis,
-                                                      int64_t* __restrict__ out_list, int ip, CoarsePlan cp) {
-  extern __shared__ __attribute__((aligned(16))) float cs_mem[];
-  float* xs = cs_mem;                       // [CQ][d]
-  float* xn = xs + CQ * d;                  // [CQ]
-  float* dist = xn + CQ;                    // [CQ][nlist]
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int64_t q0 = (int64_t)blockIdx.x * CQ;
-  for (int e = tid; e < CQ * d; e += 256) {
-    const int64_t q = q0 + e / d;
-    xs[e] = q < nq ? x[q0 * d + e] : 0.f;
-  }
-  __syncthreads();
-  if (tid < CQ) {
-    const float* xr = xs + tid * d;
-    xn[tid] = tree<K_NORM>([&](int t) { return xr[t]; }, [&](int t) { return xr[t]; }, d);
-  }
-  if (cp.T3out) {
-    const int dsub = d / cp.M;
-    const int total = cp.M * 256;
-    if (dsub == 8) {
-      // TB entries per round trip: all their codebook loads are issued before any tree
-      constexpr int TB = 4;
-      for (int e0 = tid; e0 < total; e0 += 256 * TB) {
-        float4 cw[TB][2];
-#pragma unroll
-        for (int b = 0; b < TB; b++) {
-          const float4* src = reinterpret_cast<const float4*>(cp.cb + (int64_t)min(e0 + b * 256, total - 1) * 8);
-          cw[b][0] = src[0];
-          cw[b][1] = src[1];
-        }
-#pragma unroll
-        for (int b = 0; b < TB; b++) {
-          const int e = e0 + b * 256;
-          if (e >= total) break;
-          const float* w = reinterpret_cast<const float*>(cw[b]);
-          const float* xm = xs + (e >> 8) * 8;
-#pragma unroll
-          for (int qq = 0; qq < CQ; qq++) {
-            if (q0 + qq >= nq) break;
-            const float* xq = xm + qq * d;
-            cp.T3out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
-          }
-        }
-      }
-    } else {
-      for (int e = tid; e < total; e += 256) {
-        const float* xm = xs + (e >> 8) * dsub;
-        const float* cwp = cp.cb + (int64_t)e * dsub;
-        for (int qq = 0; qq < CQ; qq++) {
-          if (q0 + qq >= nq) break;
-          const float* xq = xm + qq * d;
-          cp.T3out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
-        }
-      }
-    }
-  }
-  for (int cb0 = 0; cb0 < nlist; cb0 += 1024) {
-    const int c4 = cb0 + 4 * tid;  // first of this thread's 4 centroids
-    float acc[CQ][4];
-#pragma unroll
-    for (int qq = 0; qq < CQ; qq++)
-#pragma unroll
-      for (int u = 0; u < 4; u++) acc[qq][u] = 0.f;
-    if (c4 < nlist) {
-      // centT rows are padded to a multiple of 4 columns: branch-free float4 loads
-      const int ldc = (nlist + 3) & ~3;
-      constexpr int KB = 16;  // centroid rows in flight
-      for (int k0 = 0; k0 < d; k0 += KB) {
-        float4 cv[KB];
-#pragma unroll
-        for (int u = 0; u < KB; u++) {
-          const int kk = min(k0 + u, d - 1);
-          cv[u] = *reinterpret_cast<const float4*>(centT + (int64_t)kk * ldc + c4);
-        }
-#pragma unroll
-        for (int u = 0; u < KB; u++) {
-          if (k0 + u < d) {
-#pragma unroll
-            for (int qq = 0; qq < CQ; qq++) {
-              const float xv = xs[qq * d + k0 + u];
-              acc[qq][0] = __builtin_fmaf(xv, cv[u].x, acc[qq][0]);
-              acc[qq][1] = __builtin_fmaf(xv, cv[u].y, acc[qq][1]);
-              acc[qq][2] = __builtin_fmaf(xv, cv[u].z, acc[qq][2]);
-              acc[qq][3] = __builtin_fmaf(xv, cv[u].w, acc[qq][3]);
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();  // xn ready
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int c = c4 + u;
-      if (c < nlist) {
-        const float cnv = ip ? 0.f : cn[c];
-#pragma unroll
-        for (int qq = 0; qq < CQ; qq++) {
-          float dis;
-          if (ip) {
-            dis = -acc[qq][u];
-          } else {
-            dis = (xn[qq] + cnv) - 2.0f * acc[qq][u];
-            if (dis < 0.f) dis = 0.f;
-          }
-          dist[qq * nlist + c] = dis;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  const int64_t q = q0 + wave;
-  if (q >= nq) return;
-  const float pad = ip ? -FLT_MAX : FLT_MAX;
-  float* drow = dist + wave * nlist;  // LDS row of this wave's query
-  if constexpr (R == 1) {
-    // 16 candidates per lane per 1024-centroid block: sort in registers, 64-way
-    // merge for the block's nprobe best, fold into the running list
-    float rd = kInf;
-    int64_t ri = kSentinelId;
-    for (int base = 0; base < nlist; base += 1024) {
-      float cd[16];
-      int64_t ci[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const int cix = base + u * 64 + lane;
-        cd[u] = cix < nlist ? drow[cix] : kInf;
-        ci[u] = cix < nlist ? (int64_t)cix : kSentinelId;
-      }
-      float bd;
-      int64_t bi;
-      // drow[0, 128) is free scratch once this block's entries are in registers
-      if (nlist < 128 || !wave_select_threshold(cd, ci, nprobe, lane, drow, bd, bi)) {
-        lane_sort<16>(cd, ci);
-        wave_kway<16>(cd, ci, nprobe, lane, bd, bi);
-      }
-      if (base == 0) {
-        rd = bd;
-        ri = bi;
-      } else {
-        WaveTopK<1> tk1;
-        tk1.init(nprobe);
-        tk1.d[0] = rd;
-        tk1.id[0] = ri;
-        bulk_merge_row(tk1, bd, bi, lane);
-        rd = tk1.d[0];
-        ri = tk1.id[0];
-      }
-    }
-    if (lane < nprobe) {
-      const bool empty = ri == kSentinelId;
-      out_dis[q * nprobe + lane] = empty ? pad : (ip ? -rd : rd);
-      out_list[q * nprobe + lane] = empty ? -1 : ri;
-    }
-    if (cp.on) {  // list-major planning of this query's probes (k_plan_count's rules)
-      const int64_t l = ri;  // kSentinelId when empty: outside [lo, hi)
-      const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
-      const uint64_t um = __ballot(use);
-      const int fp = um ? (int)__builtin_ctzll(um) : 64;
-      if (lane == 0) cp.pl.tauq[q] = f2ord(kInf);
-      if (use) {
-        float d0 = rd;
-        if (ip) {
-          const float* xq = xs + wave * d;
-          const float* cl = cp.cent + l * d;
-          d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
-        }
-        plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
-      }
-    }
-    return;
-  }
-  WaveTopK<R> tk;
-  tk.init(nprobe);
-  for (int base = 0; base < nlist; base += 64) {
-    const int cix = base + lane;
-    const bool valid = cix < nlist;
-    const float v = valid ? drow[cix] : kInf;
-    const bool pass = valid && lexless(v, (int64_t)cix, tk.td, tk.ti);
-    const uint64_t mask = __ballot(pass);
-    if (!mask) continue;
-    tk.insert(mask, v, (int64_t)cix, lane);
-  }
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const int idx = r * 64 + lane;
-    if (idx < nprobe) {
-      const bool empty = tk.id[r] == kSentinelId;
-      out_dis[q * nprobe + idx] = empty ? pad : (ip ? -tk.d[r] : tk.d[r]);
-      out_list[q * nprobe + idx] = empty ? -1 : tk.id[r];
-    }
-  }
-}
 
 // ------------------------------------------------------------ row select
 template <int R>
@@ -797,6 +590,394 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
       oc[row * n + idx] = empty ? -1 : tk.id[r];
     }
   }
+}
+
+// ------------------------------------------------- coarse probe (MFMA path)
+// (key, column) packed so that unsigned 64-bit order is (key asc, column asc).
+__device__ __forceinline__ uint64_t pack_kc(float key, int col) {
+  return ((uint64_t)((uint32_t)f2ord(key) ^ 0x80000000u) << 32) | (uint32_t)col;
+}
+__device__ __forceinline__ float kc_key(uint64_t p) { return ord2f((int)((uint32_t)(p >> 32) ^ 0x80000000u)); }
+constexpr uint64_t kKcNone = ~0ull;
+
+template <int J>
+__device__ __forceinline__ uint64_t xor_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)xor_i<J>((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)xor_i<J>((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+// one compare-exchange step of the bitonic network on packed keys
+template <int KK, int J>
+__device__ __forceinline__ void kc_step(uint64_t& p, int lane) {
+  const uint64_t o = xor_u64<J>(p);
+  const bool up = KK >= 64 || (lane & KK) == 0;
+  const bool take_min = ((lane & J) == 0) == up;
+  p = ((o < p) == take_min) ? o : p;
+}
+template <int KK, int J>
+__device__ __forceinline__ void kc_steps(uint64_t& p, int lane) {
+  if constexpr (J >= 1) {
+    kc_step<KK, J>(p, lane);
+    kc_steps<KK, J / 2>(p, lane);
+  }
+}
+template <int KK = 2>
+__device__ __forceinline__ void kc_sort64(uint64_t& p, int lane) {  // ascending across the wave
+  if constexpr (KK <= 64) {
+    kc_steps<KK, KK / 2>(p, lane);
+    kc_sort64<KK * 2>(p, lane);
+  }
+}
+// run (sorted asc) := the 64 smallest of run and p (p sorted asc)
+__device__ __forceinline__ void kc_merge64(uint64_t& run, uint64_t p, int lane) {
+  const uint32_t lo = (uint32_t)rev64_i((int)(uint32_t)p);
+  const uint32_t hi = (uint32_t)rev64_i((int)(uint32_t)(p >> 32));
+  const uint64_t rev = ((uint64_t)hi << 32) | lo;
+  run = rev < run ? rev : run;  // bitonic: ascending run vs descending p
+  kc_steps<128, 32>(run, lane);
+}
+
+// Key matrix of the coarse quantizer on the matrix cores: keys[q][c] =
+// max(0, (|x_q|^2 + |c|^2) - 2 <x_q, c>) (L2) or -<x_q, c> (IP), where <.,.>
+// is accumulated by v_mfma_f32_16x16x4_f32 in ascending k, which rounds like
+// the k-ordered fmaf chain of the oracle (checked bit for bit on gfx950).
+// Workgroup = 16 queries x 256 centroids (wave w: 4 tiles of 16 centroids).
+// Workgroups past the key tiles build T3 [nq][M][256] (Faiss tree order) for
+// 16 queries x 1024 entries each, when T3out is set.
+constexpr int GQ = 16, GC = 256, GE = 1024;
+
+// rows q0..q0+15 of x into xs[16][d] (zeros past nq); all loads before the stores
+__device__ __forceinline__ void fill_rows(float* xs, const float* __restrict__ x, int64_t q0, int64_t nq, int d,
+                                          int tid) {
+  const int64_t n = (int64_t)min<int64_t>(GQ, nq - q0) * d;
+  if ((d & 3) == 0) {
+    const float4* src = reinterpret_cast<const float4*>(x + q0 * d);
+    float4* dst = reinterpret_cast<float4*>(xs);
+    const int n4 = GQ * d / 4;
+    constexpr int U = 4;
+    for (int e0 = tid; e0 < n4; e0 += 256 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int e = e0 + u * 256;
+        v[u] = 4 * (int64_t)e < n ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (e0 + u * 256 < n4) dst[e0 + u * 256] = v[u];
+    }
+  } else {
+    for (int e = tid; e < GQ * d; e += 256) xs[e] = e < n ? x[q0 * d + e] : 0.f;
+  }
+}
+// the same rows transposed into xs[dk][16] (k-major; zeros past nq and d)
+__device__ __forceinline__ void fill_cols(float* xs, const float* __restrict__ x, int64_t q0, int64_t nq, int d,
+                                          int dk, int tid) {
+  if ((d & 3) == 0 && d <= 1024) {
+    const int nk4 = dk / 4;  // thread k4: elements 4 k4 .. 4 k4 + 3 of the 16 rows
+    for (int k4 = tid; k4 < nk4; k4 += 256) {
+      float4 r[GQ];
+#pragma unroll
+      for (int i = 0; i < GQ; i++)
+        r[i] = (q0 + i < nq && 4 * k4 < d) ? reinterpret_cast<const float4*>(x + (q0 + i) * d)[k4]
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4* row = reinterpret_cast<float4*>(xs + 4 * k4 * GQ);  // 4 k-rows of 16 floats
+#pragma unroll
+      for (int i4 = 0; i4 < GQ / 4; i4++) {
+        row[0 * 4 + i4] = make_float4(r[4 * i4].x, r[4 * i4 + 1].x, r[4 * i4 + 2].x, r[4 * i4 + 3].x);
+        row[1 * 4 + i4] = make_float4(r[4 * i4].y, r[4 * i4 + 1].y, r[4 * i4 + 2].y, r[4 * i4 + 3].y);
+        row[2 * 4 + i4] = make_float4(r[4 * i4].z, r[4 * i4 + 1].z, r[4 * i4 + 2].z, r[4 * i4 + 3].z);
+        row[3 * 4 + i4] = make_float4(r[4 * i4].w, r[4 * i4 + 1].w, r[4 * i4 + 2].w, r[4 * i4 + 3].w);
+      }
+    }
+  } else {
+    for (int e = tid; e < GQ * dk; e += 256) {
+      const int i = e / dk, k = e % dk;
+      xs[k * GQ + i] = (q0 + i < nq && k < d) ? x[(q0 + i) * d + k] : 0.f;
+    }
+  }
+}
+
+struct CoarseT3 {
+  float* out = nullptr;  // [nq][M * 256]
+  const float* cb = nullptr;
+  int M = 0;
+  int nblk = 0;  // T3 workgroups
+};
+
+__global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
+                                                     const float* __restrict__ centT, int ldc,
+                                                     const float* __restrict__ cn, int nlist,
+                                                     float* __restrict__ keys, int ip, int ngemm, CoarseT3 t3) {
+  extern __shared__ __attribute__((aligned(16))) float g_lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  CDIAG(0);
+#ifdef DIAG_G_NOT3
+  if ((int)blockIdx.x >= ngemm) return;
+#endif
+#ifdef DIAG_G_NOKEYS
+  if ((int)blockIdx.x < ngemm) return;
+#endif
+  if ((int)blockIdx.x >= ngemm) {
+    // ---- T3 role: 16 queries x 1024 entries
+    const int tb = blockIdx.x - ngemm;
+    const int total = t3.M * 256;
+    const int ne = (total + GE - 1) / GE;
+    const int64_t q0 = (int64_t)(tb / ne) * GQ;
+    const int e0 = (tb % ne) * GE;
+    float* xs = g_lds;  // [GQ][d]
+    fill_rows(xs, x, q0, nq, d, tid);
+    __syncthreads();
+    CDIAG(1);
+    const int dsub = d / t3.M;
+    const int nqq = (int)min<int64_t>(GQ, nq - q0);
+    if (dsub == 8) {
+      float4 cw[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int e = min(e0 + u * 256 + tid, total - 1);
+        const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
+        cw[u][0] = src[0];
+        cw[u][1] = src[1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int e = e0 + u * 256 + tid;
+        if (e >= total) break;
+        const float* w = reinterpret_cast<const float*>(cw[u]);
+        const float* xm = xs + (e >> 8) * 8;
+        // 4 queries at a time: their sub-vectors are read before any tree
+        for (int g0 = 0; g0 < nqq; g0 += 4) {
+          float4 xv[4][2];
+#pragma unroll
+          for (int h = 0; h < 4; h++) {
+            const float4* src = reinterpret_cast<const float4*>(xm + min(g0 + h, GQ - 1) * d);
+            xv[h][0] = src[0];
+            xv[h][1] = src[1];
+          }
+#pragma unroll
+          for (int h = 0; h < 4; h++) {
+            if (g0 + h >= nqq) break;
+            const float* xq = reinterpret_cast<const float*>(xv[h]);
+#ifdef DIAG_G_NOSTORE
+            const float tv = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
+            asm volatile("" ::"v"(tv));
+#else
+            t3.out[(q0 + g0 + h) * total + e] =
+                tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
+#endif
+          }
+        }
+      }
+    } else {
+      for (int u = 0; u < 4; u++) {
+        const int e = e0 + u * 256 + tid;
+        if (e >= total) break;
+        const float* xm = xs + (e >> 8) * dsub;
+        const float* cwp = t3.cb + (int64_t)e * dsub;
+        for (int qq = 0; qq < nqq; qq++) {
+          const float* xq = xm + qq * d;
+          t3.out[(q0 + qq) * total + e] =
+              tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
+        }
+      }
+    }
+#ifdef DIAG_CSTAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    CDIAG(5);
+    return;
+  }
+  // ---- key tile: 16 queries x 256 centroids
+  const int nct = (nlist + GC - 1) / GC;
+  const int64_t q0 = (int64_t)(blockIdx.x / nct) * GQ;
+  const int c0 = (blockIdx.x % nct) * GC + wave * 64;
+  const int dk = (d + 63) & ~63;  // A rows, zero-padded to whole double chunks
+  float* xs = g_lds;              // [dk][GQ]: the A operand, k-major
+  float* xn = xs + dk * GQ;       // [GQ]
+  fill_cols(xs, x, q0, nq, d, dk, tid);
+  __syncthreads();
+  CDIAG(1);
+  // |x_q|^2 in Faiss tree order: with d % 8 == 0 the 8 lane sums of each query
+  // are 8 independent sequential chains (threads i * 8 + j), folded by 16 threads
+  float* a8 = xn + GQ;  // [GQ][8]
+  if (d % 8 == 0) {
+    if (tid < GQ * 8) {
+      const int i = tid >> 3, j = tid & 7;
+      float acc8 = 0.f;
+      for (int k = j; k < d; k += 8) {
+        const float v = xs[k * GQ + i];
+        acc8 = acc8 + v * v;
+      }
+      a8[i * 8 + j] = acc8;
+    }
+    __syncthreads();
+    if (tid < GQ) {
+      const float* r = a8 + tid * 8;
+      const float h0 = (r[4] + r[0]) + (r[5] + r[1]);
+      const float h1 = (r[6] + r[2]) + (r[7] + r[3]);
+      xn[tid] = h0 + h1;
+    }
+  } else if (tid < GQ) {
+    xn[tid] = tree<K_NORM>([&](int t) { return xs[t * GQ + tid]; }, [&](int t) { return xs[t * GQ + tid]; }, d);
+  }
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  const int i16 = lane & 15, k4 = lane >> 4;
+  const float* bcol[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) bcol[t] = centT + min(c0 + t * 16 + i16, nlist - 1);  // clamped columns
+  // B operand rows, 8 k-steps (32 k) per chunk, two chunks in flight.  Rows
+  // past d are clamped to row d - 1: their A entries are 0 and fma(0, b, acc)
+  // == acc for every finite b (acc is never -0).
+  constexpr int KS = 8;
+  float b0[KS][4], b1[KS][4];
+  auto load_b = [&](int k0, float (&b)[KS][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < KS; j++) {
+      const int64_t kr = min(k0 + 4 * j + k4, d - 1);
+#pragma unroll
+      for (int t = 0; t < 4; t++) b[j][t] = bcol[t][kr * ldc];
+    }
+  };
+  auto mma = [&](int k0, const float (&b)[KS][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < KS; j++) {
+      const float av = xs[(k0 + 4 * j + k4) * GQ + i16];
+#pragma unroll
+      for (int t = 0; t < 4; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
+    }
+  };
+  load_b(0, b0);
+  for (int k0 = 0; k0 < dk; k0 += 64) {
+    load_b(k0 + 32, b1);
+    mma(k0, b0);
+    load_b(k0 + 64, b0);  // past the end on the last pass: clamped, unused
+    mma(k0 + 32, b1);
+  }
+  CDIAG(2);
+  __syncthreads();  // xn
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int c = c0 + t * 16 + i16;
+    if (c >= nlist) continue;
+    const float cnv = ip ? 0.f : cn[c];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int i = k4 * 4 + r;
+      if (q0 + i >= nq) continue;
+      float v;
+      if (ip) {
+        v = -acc[t][r];
+      } else {
+        v = (xn[i] + cnv) - 2.0f * acc[t][r];
+        if (v < 0.f) v = 0.f;
+      }
+      keys[(q0 + i) * nlist + c] = v;
+    }
+  }
+#ifdef DIAG_CSTAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+  CDIAG(5);
+}
+
+// Per query (one wave): the nprobe (<= 64) smallest keys of its row, by
+// (key, list); per block of 1024 lists the candidates are cut by the
+// nprobe-th smallest of the 64 lane minima (those minima are nprobe distinct
+// keys, so every member of the block's top-nprobe is at or below it), sorted
+// once and merged into the running list.  With `cp.on`, the epilogue plans
+// the batch exactly as k_coarse_fused did (first usable probe, tau reset,
+// bucket entries with the scan's dis0).
+__global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__ keys, int64_t nq, int nlist,
+                                                       int nprobe, float* __restrict__ out_dis,
+                                                       int64_t* __restrict__ out_list, int ip,
+                                                       const float* __restrict__ x, int d, CoarsePlan cp) {
+  __shared__ uint64_t scratch[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+  if (q >= nq) return;  // wave-uniform
+  const float* row = keys + q * nlist;
+  const uint64_t lt = (1ull << lane) - 1;
+  uint64_t run = kKcNone;
+  SDIAG(0);
+  for (int base = 0; base < nlist; base += 1024) {
+    float v[16];
+    float m = kInf;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int c = base + u * 64 + lane;
+      v[u] = c < nlist ? row[c] : kInf;
+      m = fminf(m, v[u]);
+    }
+#ifdef DIAG_CSTAMPS
+    asm volatile("" ::"v"(m));
+#endif
+    SDIAG(1);
+    const float T = wave_kth_smallest(m, nprobe, lane);
+    SDIAG(2);
+    int total = 0;
+    bool fits = true;
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int c = base + u * 64 + lane;
+      const bool pass = c < nlist && v[u] <= T;
+      const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+      const int pos = total + __popcll(mk & lt);
+      if (pass && pos < 64) scratch[wave][pos] = pack_kc(v[u], c);
+      total += __popcll(mk);
+    }
+    fits = total <= 64;
+    uint64_t p;
+    if (fits) {
+      __builtin_amdgcn_wave_barrier();
+      p = lane < total ? scratch[wave][lane] : kKcNone;
+      kc_sort64(p, lane);
+      kc_merge64(run, p, lane);
+    } else {  // many ties at the cut (rare): every 64-key slice of the block
+#pragma unroll
+      for (int u = 0; u < 16; u++) {
+        const int c = base + u * 64 + lane;
+        p = c < nlist ? pack_kc(v[u], c) : kKcNone;
+        kc_sort64(p, lane);
+        kc_merge64(run, p, lane);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // scratch reuse
+  }
+  SDIAG(3);
+  const bool empty = run == kKcNone;
+  const float rd = kc_key(run);
+  const int64_t ri = empty ? kSentinelId : (int64_t)(uint32_t)run;
+  if (lane < nprobe) {
+    out_dis[q * nprobe + lane] = empty ? (ip ? -FLT_MAX : FLT_MAX) : (ip ? -rd : rd);
+    out_list[q * nprobe + lane] = empty ? -1 : ri;
+  }
+  if (cp.on) {  // list-major planning of this query's probes (k_plan_count's rules)
+    const int64_t l = ri;  // kSentinelId when empty: outside [lo, hi)
+    const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
+    const uint64_t um = __ballot(use);
+    const int fp = um ? (int)__builtin_ctzll(um) : 64;
+    if (lane == 0) cp.pl.tauq[q] = f2ord(kInf);
+    if (use) {
+      float d0 = rd;
+      if (ip) {
+        const float* xq = x + q * d;
+        const float* cl = cp.cent + l * d;
+        d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
+      }
+      plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
+    }
+  }
+#ifdef DIAG_CSTAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+  SDIAG(5);
 }
 
 // -------------------------------------------------------------- PQ tables
@@ -1184,8 +1365,6 @@ struct Item {
 constexpr int QCAP = 256;  // per-wave candidate queue entries
 
 #ifdef DIAG_STAMPS  // diagnostic builds only (profiles/diag_stamps.py): per-item phase stamps
-constexpr int kDiagWG = 1024, kDiagItems = 64, kDiagSlots = 8;
-__device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
 #define DIAG(slot, v)                                                                                \
   do {                                                                                               \
     if (tid == 0 && blockIdx.x < kDiagWG && it_no < kDiagItems)                                      \
@@ -1203,8 +1382,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   constexpr int LUTN = M * 256;
   constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table
   __shared__ __attribute__((aligned(16))) V lut[LUTN];
-  __shared__ float qd[4][QCAP];
-  __shared__ int32_t qi[4][QCAP];  // (position in the list << 2) | g
+  constexpr int QG = QCAP / G;  // queue entries per wave and pair
+  __shared__ float qd[4][QCAP];    // [wave][g][QG]
+  __shared__ int32_t qi[4][QCAP];  // positions in the list
   __shared__ int s_next;
   __shared__ int32_t s_wb[G];  // the item's per-query bounds found by its waves (ordered ints)
 
@@ -1248,6 +1428,49 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   if (cur >= 0) unpack(fetch_rec(cur));
   int it_no = 0;
   (void)it_no;
+  // The next item's first loads -- its queries' running k-th keys (a stale
+  // value is only a looser bound) and the first group of LUT rows -- are
+  // issued at the end of the previous item's scan, before its partial writes,
+  // so that they arrive while those and the barrier run.  Later LUT row groups
+  // (M > 16) are software-pipelined in the build; the codes are loaded at the
+  // item start, in flight during the LUT stores.
+  constexpr int U = NV < 4 ? NV : 4;
+  constexpr int NG = NV / U;
+  static_assert(NV % U == 0, "LUT rows per thread");
+  int tq[G];
+  CodeWords<M> cw[JB];
+  float4 b1[2][U], b3[2][U][G];
+  auto t3row = [&](int g) __attribute__((always_inline)) {
+    return reinterpret_cast<const float4*>(a.T3 + (int64_t)((g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe) * LUTN);
+  };
+  // IP has no T1: read (and ignore) a T3 row instead, so that every load is unconditional
+  auto t1row = [&]() __attribute__((always_inline)) {
+    return ip ? t3row(0) : reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
+  };
+  auto fetch = [&](int u, int buf) __attribute__((always_inline)) {
+    const float4* T1l = t1row();
+#pragma unroll
+    for (int e = 0; e < U; e++) {
+      const int v = (u * U + e) * 256 + tid;
+      b1[buf][e] = T1l[v];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+#ifdef DIAG_NOT3
+        b3[buf][e][g] = make_float4(g, v, 0, 1);
+#else
+        b3[buf][e][g] = t3row(g)[v];
+#endif
+      }
+    }
+  };
+  auto issue = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < G; g++) tq[g] = pl.tauq[(g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe];
+    fetch(0, 0);
+  };
+  // (with R > 1 the larger top-k state leaves no registers for that: issued at the item start)
+  constexpr bool kEarly = false;  // measured: no gain at C2 (register pressure)
+  if (kEarly && cur >= 0) issue();
   while (cur >= 0) {
     __syncthreads();  // (A) every wave is done with the LUT of the previous item, and has read s_next
     DIAG(0, __builtin_amdgcn_s_memtime());
@@ -1255,14 +1478,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     // other lanes: no merge copy that would wait for the atomic right here)
     int tnext;
     if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);
-    // the queries' running k-th keys, read with the LUT rows (a stale value is only a looser bound)
-    int tq[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) tq[g] = pl.tauq[(g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe];
-    // the item's first JB x 256 codes, issued with the LUT rows (one round trip for both)
+    if constexpr (!kEarly) issue();
     const int n = it.n;
     const uint8_t* lc = a.codes + it.beg * M;
-    CodeWords<M> cw[JB];
+    // the item's first JB x 256 codes: in flight during the LUT stores
 #pragma unroll
     for (int j = 0; j < JB; j++) {
       const int i = j * 256 + wave * 64 + lane;
@@ -1272,52 +1491,23 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
 #endif
     }
-    {  // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0.
-      // Software-pipelined in groups of U float4 rows per thread: the loads of
-      // group u + 1 are in flight while group u is combined and stored.
-      const float4* T3q[G];
+    // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
 #pragma unroll
-      for (int g = 0; g < G; g++)
-        T3q[g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)((g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe) * LUTN);
-      // IP has no T1: read (and ignore) a T3 row instead, so that every load is unconditional
-      const float4* T1l = ip ? T3q[0] : reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l * LUTN);
-      constexpr int U = NV < 4 ? NV : 4;
-      constexpr int NG = NV / U;
-      static_assert(NV % U == 0, "LUT rows per thread");
-      float4 b1[2][U], b3[2][U][G];
-      auto fetch = [&](int u, int buf) __attribute__((always_inline)) {
+    for (int u = 0; u < NG; u++) {
+      if (u + 1 < NG) fetch(u + 1, (u + 1) & 1);
 #pragma unroll
-        for (int e = 0; e < U; e++) {
-          const int v = (u * U + e) * 256 + tid;
-          b1[buf][e] = T1l[v];
+      for (int e = 0; e < U; e++) {
+        const int v = (u * U + e) * 256 + tid;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          V o;
 #pragma unroll
           for (int g = 0; g < G; g++) {
-#ifdef DIAG_NOT3
-            b3[buf][e][g] = make_float4(g, v, 0, 1);
-#else
-            b3[buf][e][g] = T3q[g][v];
-#endif
+            const float x3 = comp(b3[u & 1][e][g], c);
+            const float lv = ip ? -x3 : comp(b1[u & 1][e], c) + (-2.0f * x3);
+            setc(o, g, g < it.cnt ? lv : 0.f);
           }
-        }
-      };
-      fetch(0, 0);
-#pragma unroll
-      for (int u = 0; u < NG; u++) {
-        if (u + 1 < NG) fetch(u + 1, (u + 1) & 1);
-#pragma unroll
-        for (int e = 0; e < U; e++) {
-          const int v = (u * U + e) * 256 + tid;
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            V o;
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              const float x3 = comp(b3[u & 1][e][g], c);
-              const float lv = ip ? -x3 : comp(b1[u & 1][e], c) + (-2.0f * x3);
-              setc(o, g, g < it.cnt ? lv : 0.f);
-            }
-            lut[4 * v + c] = o;
-          }
+          lut[4 * v + c] = o;
         }
       }
     }
@@ -1341,42 +1531,61 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     WaveTopK<R, int> tk[G];
 #pragma unroll
     for (int g = 0; g < G; g++) tk[g].init(k);
-    int qn = 0;  // this wave's queue fill (wave-uniform)
+    int qn[G];  // this wave's queue fills (wave-uniform)
+#pragma unroll
+    for (int g = 0; g < G; g++) qn[g] = 0;
 #ifdef DIAG_STAMPS
     int npush = 0;
     uint64_t tdrain = 0;
+    uint64_t nbulk = 0, ninsert = 0, ndrain = 0;
 #ifdef DIAG_FINE
     asm volatile("" ::"v"(bound[0]), "v"(bound[G - 1]));
     DIAG(6, __builtin_amdgcn_s_memtime());
 #endif
 #endif
 
-    // drain the queue into the per-query top-k lists and publish the bounds
+    // drain the queues into the per-query top-k lists and publish the bounds
     auto drain = [&]() __attribute__((always_inline)) {
-      for (int b0 = 0; b0 < qn; b0 += 64) {
-        const int e = b0 + lane;
-        const float cd = e < qn ? qd[wave][e] : kInf;
-        const int cidx = e < qn ? qi[wave][e] : 0;
-        const int pos = cidx >> 2;
-        const int cg = cidx & 3;
+#ifdef DIAG_DRAINCNT
+      ndrain++;
+#endif
+      for (int b0 = 0; b0 < QG; b0 += 64) {
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < G; g++) any = any || b0 < qn[g];
+        if (!any) break;
 #pragma unroll
         for (int g = 0; g < G; g++) {
-          const bool p = e < qn && cg == g && lexless(cd, pos, tk[g].td, tk[g].ti);
+          if (b0 >= qn[g]) continue;
+          const int e = b0 + lane;
+          const float cdg = e < qn[g] ? qd[wave][g * QG + e] : kInf;
+          const int cpg = e < qn[g] ? qi[wave][g * QG + e] : id_none<int>();
+          const bool p = lexless(cdg, cpg, tk[g].td, tk[g].ti);
           const uint64_t mk = __ballot(p);
-          if (mk) {
-            if constexpr (R == 1) {
-              if (__popcll(mk) > 6)
-                bulk_merge_row(tk[g], p ? cd : kInf, p ? pos : id_none<int>(), lane);
-              else
-                tk[g].insert(mk, cd, pos, lane);
-            } else {
-              tk[g].insert(mk, cd, pos, lane);
-            }
-            bound[g] = fminf(bound[g], tk[g].td);
+          if (!mk) continue;
+#ifdef DIAG_DRAINCNT
+          const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
+          if constexpr (R == 1) {
+            if (k <= 16 && qn[g] - b0 <= 16 && __popcll(mk) > 1)
+              row16_merge(tk[g], p ? cdg : kInf, p ? cpg : id_none<int>(), lane);
+            else if (__popcll(mk) > 6)
+              bulk_merge_row(tk[g], p ? cdg : kInf, p ? cpg : id_none<int>(), lane);
+            else
+              tk[g].insert(mk, cdg, cpg, lane);
+          } else {
+            tk[g].insert(mk, cdg, cpg, lane);
           }
+#ifdef DIAG_DRAINCNT
+          asm volatile("" ::"v"(tk[g].d[0]), "s"(tk[g].td));
+          const uint64_t tb1 = __builtin_amdgcn_s_memtime() - tb0;
+          if (__popcll(mk) > 1) nbulk += tb1; else ninsert += tb1;
+#endif
+          bound[g] = fminf(bound[g], tk[g].td);
         }
       }
-      qn = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) qn[g] = 0;
       loose = false;
 #pragma unroll
       for (int g = 0; g < G; g++) {
@@ -1477,6 +1686,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         loose = loose || bound[g] == kInf;
       }
       int t = 0;
+      bool pend = false;  // a drain requested by the last chunk
       while (true) {
         int stop = tn;       // first chunk not yet admitted
         bool want = false;   // drain requested
@@ -1493,8 +1703,11 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
               mk[g] = __builtin_amdgcn_ballot_w64(valid && dis[j][g] <= bound[g]);
               tj += __popcll(mk[g]);
             }
+            bool full = false;
+#pragma unroll
+            for (int g = 0; g < G; g++) full = full || qn[g] + __popcll(mk[g]) > QG;
             if (tj > 0) {
-              if (qn + tj > QCAP) {  // no room: drain first, then redo this chunk
+              if (full) {  // no room: drain first, then redo this chunk
                 stop = j;
                 want = true;
                 go = false;
@@ -1502,11 +1715,11 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
                 for (int g = 0; g < G; g++) {
                   if ((mk[g] >> lane) & 1) {
-                    const int sl = qn + __popcll(mk[g] & lanemask_lt);
+                    const int sl = g * QG + qn[g] + __popcll(mk[g] & lanemask_lt);
                     qd[wave][sl] = dis[j][g];
-                    qi[wave][sl] = (i << 2) | g;
+                    qi[wave][sl] = i;
                   }
-                  qn += __popcll(mk[g]);
+                  qn[g] += __popcll(mk[g]);
                 }
 #ifdef DIAG_STAMPS
                 npush += tj;
@@ -1520,17 +1733,30 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
             }
           }
         }
-        if (want || (stop >= tn && last_sb && qn > 0)) {
-#ifdef DIAG_STAMPS
-          const uint64_t td0 = __builtin_amdgcn_s_memtime();
-          drain();
-          tdrain += __builtin_amdgcn_s_memtime() - td0;
-#else
-          drain();
-#endif
+        if (stop >= tn) {  // a drain wanted here is left to the end of the super-batch
+          pend = want;
+          break;
         }
-        if (stop >= tn) break;
+#ifdef DIAG_STAMPS
+        const uint64_t td0 = __builtin_amdgcn_s_memtime();
+        drain();
+        tdrain += __builtin_amdgcn_s_memtime() - td0;
+#else
+        drain();
+#endif
         t = stop;
+      }
+      bool queued = false;
+#pragma unroll
+      for (int g = 0; g < G; g++) queued = queued || qn[g] > 0;
+      if (pend || (last_sb && queued)) {
+#ifdef DIAG_STAMPS
+        const uint64_t td0 = __builtin_amdgcn_s_memtime();
+        drain();
+        tdrain += __builtin_amdgcn_s_memtime() - td0;
+#else
+        drain();
+#endif
       }
     }
     DIAG(2, __builtin_amdgcn_s_memtime());
@@ -1541,12 +1767,18 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     DIAG(4, n);
     DIAG(5, ci.cnt | (ci.kind << 8));
 #ifndef DIAG_FINE
+#ifdef DIAG_DRAINCNT
+    DIAG(6, (nbulk & 0xFFFFFF) | ((ninsert & 0xFFFFFF) << 24) | (ndrain << 48));
+#else
     DIAG(6, npush);
 #endif
 #endif
+#endif
 
-    // the next item's fields (before the stores below, which a later wait would also cover)
-    if (nxt >= 0) unpack(nrec);
+    if (nxt >= 0) {  // the next item's fields; with kEarly its first loads start here
+      unpack(nrec);
+      if constexpr (kEarly) issue();
+    }
     // each wave writes its own sorted partial list per pair (merged by k_merge_probes)
 #pragma unroll
     for (int g = 0; g < G; g++) {
@@ -1582,11 +1814,17 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   const int np = a.nprobe;
   const float pad = a.ip ? -FLT_MAX : FLT_MAX;
   const float sgn = a.ip ? -1.f : 1.f;  // key -> reported value
-  if (R == 1 && k <= 16 && np * 4 <= 64) {
-    // fast path: lane j owns partial list j = (probe j/4, wave j%4), already
-    // sorted by (key, label); one 64-way merge
-    float d[16];
-    int64_t id[16];
+  if (R == 1 && np * 4 <= 64) {
+    // fast path: lane j owns partial list j = (probe j/4, wave j%4), sorted by
+    // (key, label).  T = the k-th smallest list head bounds the k-th key (k
+    // distinct entries are at or below it), so only the list prefixes <= T are
+    // candidates: they are compacted into one slot per lane, their labels
+    // looked up, and one 64-lane sort yields the top-k.
+    __shared__ float sd[4][64];
+    __shared__ int64_t sp[4][64];
+    const int wave = threadIdx.x >> 6;
+    constexpr int U = 16;
+    float d[U];
     const int p = min(lane >> 2, np - 1);
     bool scanned = false;
     if ((lane >> 2) < np) {
@@ -1594,31 +1832,46 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
     }
     const int64_t base = ((q * np + p) * 4 + (lane & 3)) * k;
-    // unconditional, clamped loads (no divergent branch around them)
-    int64_t pos[16];
+    // unconditional, clamped loads (no divergent branch around them); slots of
+    // unscanned probes (empty or foreign lists, lanes past nprobe) were never
+    // written this batch: their contents are stale and must not be used
+    int64_t pos[U];
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
+    for (int u = 0; u < U; u++) {
       pos[u] = pl.partI[base + min(u, k - 1)];
       d[u] = pl.partD[base + min(u, k - 1)];
     }
+    bool ok[U];
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      // slots of unscanned probes (empty or foreign lists, lanes past nprobe) were never
-      // written this batch: their positions are stale memory and must not be dereferenced
-      const bool ok = scanned && u < k && pos[u] >= 0;
-      const int64_t lab = a.ids[ok ? pos[u] : 0];
-      id[u] = ok ? lab : kSentinelId;
-      d[u] = ok ? d[u] : kInf;
+    for (int u = 0; u < U; u++) ok[u] = scanned && u < k && pos[u] >= 0;
+    const float T = wave_kth_smallest(ok[0] ? d[0] : kInf, k, lane);
+    const uint64_t lt = (1ull << lane) - 1;
+    int total = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const bool pass = ok[u] && d[u] <= T;
+      const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+      const int at = total + __popcll(mk & lt);
+      if (pass && at < 64) {
+        sd[wave][at] = d[u];
+        sp[wave][at] = pos[u];
+      }
+      total += __popcll(mk);
     }
-    float od;
-    int64_t oi;
-    wave_kway<16>(d, id, k, lane, od, oi);
-    if (lane < k) {
-      const bool empty = oi == kSentinelId;
-      a.outD[q * k + lane] = empty ? pad : sgn * od;
-      a.outI[q * k + lane] = empty ? -1 : oi;
+    // a list whose 16 loaded entries all pass may hold more candidates
+    const bool cut = k > U && __builtin_amdgcn_ballot_w64(ok[U - 1] && d[U - 1] <= T) != 0;
+    if (T < kInf && total <= 64 && !cut) {
+      __builtin_amdgcn_wave_barrier();
+      float cd = lane < total ? sd[wave][lane] : kInf;
+      int64_t ci = lane < total ? a.ids[sp[wave][lane]] : kSentinelId;
+      bitonic_sort64<2>(cd, ci, lane);
+      if (lane < k) {
+        const bool empty = ci == kSentinelId;
+        a.outD[q * k + lane] = empty ? pad : sgn * cd;
+        a.outI[q * k + lane] = empty ? -1 : ci;
+      }
+      return;
     }
-    return;
   }
   WaveTopK<R> tk;
   tk.init(k);
@@ -1716,7 +1969,6 @@ inline unsigned nblocks(int64_t n, int per) { return (unsigned)((n + per - 1) / 
 
 inline int rows_for(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : k <= 256 ? 4 : k <= 512 ? 8 : 16; }
 
-size_t coarse_smem(int nlist, int d) { return sizeof(float) * (CQ * (size_t)d + CQ + (size_t)CQ * nlist); }
 
 }  // namespace
 
@@ -1746,18 +1998,38 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
   }
 }
 
-bool coarse_fused_ok(int nlist, int nprobe, int d) {
-  (void)nprobe;
-  return nlist <= kCoarseFusedMax && coarse_smem(nlist, d) <= 160 * 1024;
+void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
+                        float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M) {
+  if (nq <= 0) return;
+  const unsigned nqb = nblocks(nq, GQ);
+  const int ngemm = (int)(nqb * nblocks(nlist, GC));
+  CoarseT3 t3;
+  if (T3out && M > 0 && d % M == 0) {
+    t3.out = T3out;
+    t3.cb = cb;
+    t3.M = M;
+    t3.nblk = (int)(nqb * nblocks((int64_t)M * 256, GE));
+  }
+  const size_t smem = sizeof(float) * std::max<size_t>((size_t)GQ * ((d + 63) & ~63) + GQ * 9, (size_t)GQ * d);
+  if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device
+    static uint64_t attr_done = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 64 && !(attr_done & (1ull << dev))) {
+      (void)hipFuncSetAttribute((const void*)k_coarse_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_done |= 1ull << dev;
+    }
+  }
+  hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
+                     (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
 }
 
-void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                         int nprobe, float* out_dis, int64_t* out_list, hipStream_t s, bool ip, const ListPlan* plan,
-                         const int64_t* list_off, int lo, int hi, const float* cent, float* T3out, const float* cb,
-                         int M) {
+void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, float* out_dis, int64_t* out_list,
+                          hipStream_t s, bool ip, const ListPlan* plan, const int64_t* list_off, int lo, int hi,
+                          const float* x, const float* cent, int d) {
   if (nq <= 0) return;
   CoarsePlan cp;
-  if (plan && nprobe <= 64) {
+  if (plan) {
     cp.pl = *plan;
     cp.on = 1;
     cp.list_off = list_off;
@@ -1765,34 +2037,8 @@ void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, 
     cp.hi = hi;
     cp.cent = cent;
   }
-  if (T3out && M > 0 && d % M == 0) {
-    cp.T3out = T3out;
-    cp.cb = cb;
-    cp.M = M;
-  }
-  const size_t smem = coarse_smem(nlist, d);
-  const dim3 grid(nblocks(nq, CQ));
-  // dynamic LDS above 64 KiB must be opted into, per device (function attributes are per device)
-  static uint64_t attr_done = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if (dev < 64 && !(attr_done & (1ull << dev))) {
-    const int lim = 160 * 1024;
-    (void)hipFuncSetAttribute((const void*)k_coarse_fused<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void*)k_coarse_fused<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void*)k_coarse_fused<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void*)k_coarse_fused<8>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    (void)hipFuncSetAttribute((const void*)k_coarse_fused<16>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    attr_done |= 1ull << dev;
-  }
-  const int ipi = ip ? 1 : 0;
-  switch (rows_for(nprobe)) {
-    case 1: hipLaunchKernelGGL(k_coarse_fused<1>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
-    case 2: hipLaunchKernelGGL(k_coarse_fused<2>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
-    case 4: hipLaunchKernelGGL(k_coarse_fused<4>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
-    case 8: hipLaunchKernelGGL(k_coarse_fused<8>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
-    default: hipLaunchKernelGGL(k_coarse_fused<16>, grid, dim3(256), smem, s, x, nq, d, centT, cn, nlist, nprobe, out_dis, out_list, ipi, cp); break;
-  }
+  hipLaunchKernelGGL(k_coarse_select, dim3(nblocks(nq, 4)), dim3(256), 0, s, keys, nq, nlist, nprobe, out_dis,
+                     out_list, ip ? 1 : 0, x, d, cp);
 }
 
 void launch_ip_table(const float* x, int64_t n, int d, const float* cb, int M, int ksub, float* out,
@@ -1915,7 +2161,7 @@ void launch_merge_topk(int S, int64_t n, int k, const float* Din, const int64_t*
 
 }  // namespace chivf
 
-#ifdef DIAG_STAMPS
+#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS)
 extern "C" int ivfpq_diag_stamps(void* out, size_t bytes) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(chivf::g_diag), bytes) != hipSuccess) return -1;
   static uint64_t zeros[chivf::kDiagWG * chivf::kDiagItems * chivf::kDiagSlots];

@@ -68,6 +68,10 @@ def main():
         sc = (t2 - t1)[sel]
         if not os.environ.get("FINE"):
             print(f"   drain cycles (wave 0) mean {tau[sel].mean():.0f} p50 {np.median(tau[sel]):.0f}")
+        if os.environ.get("DRAINCNT"):
+            pv = push[sel]
+            print(f"   drains/item {(pv >> 48).mean():.2f}  bulk-merge cycles/item {(pv & 0xFFFFFF).mean():.0f}  "
+                  f"insert cycles/item {((pv >> 24) & 0xFFFFFF).mean():.0f}")
         print(f"   scan cycles per code-pair {sc.sum() / (n[sel] * cnt[sel]).sum():.2f}, per code {sc.sum() / n[sel].sum():.2f}")
     first = np.where(valid, t0, np.iinfo(np.int64).max).min(1)
     last = np.where(valid, t3, 0).max(1)
