@@ -96,9 +96,11 @@ __device__ __forceinline__ float tree(FX fx, FY fy, int d) {
   return h0 + h1;
 }
 
+// Branch-free (bitwise, not short-circuit) so that the networks below compile
+// to compare masks and selects instead of divergent branches.
 template <class T>
 __device__ __forceinline__ bool lexless(float ad, T ai, float bd, T bi) {
-  return ad < bd || (ad == bd && ai < bi);
+  return (ad < bd) | ((ad == bd) & (ai < bi));
 }
 
 __device__ __forceinline__ float readlane_f(float v, int lane) {
@@ -144,14 +146,12 @@ __device__ __forceinline__ int rev16_i(int v) { return dmov<0x140>(v); }
 
 // Candidate ids: int64 labels / global positions, or int32 positions inside one
 // list (the list scan): half the cross-lane traffic of the top-k network.
-__device__ __forceinline__ int id_readlane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ int64_t id_readlane(int64_t v, int lane) {
   const uint64_t u = (uint64_t)v;
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ int id_shr1(int old, int v) { return dpp_shr1_i(old, v); }
 __device__ __forceinline__ int64_t id_shr1(int64_t old, int64_t v) {
   const uint64_t uo = (uint64_t)old, uv = (uint64_t)v;
   const uint32_t lo = (uint32_t)dpp_shr1_i((int)(uint32_t)uo, (int)(uint32_t)uv);
@@ -160,7 +160,6 @@ __device__ __forceinline__ int64_t id_shr1(int64_t old, int64_t v) {
 }
 template <int J>
 __device__ __forceinline__ int id_xor(int v) { return xor_i<J>(v); }
-__device__ __forceinline__ int id_rev64(int v) { return rev64_i(v); }
 __device__ __forceinline__ int64_t id_rev64(int64_t v) {
   const uint64_t u = (uint64_t)v;
   const uint32_t lo = (uint32_t)rev64_i((int)(uint32_t)u);
@@ -173,6 +172,16 @@ __device__ __forceinline__ int64_t id_xor(int64_t v) {
   const uint32_t lo = (uint32_t)xor_i<J>((int)(uint32_t)u);
   const uint32_t hi = (uint32_t)xor_i<J>((int)(uint32_t)(u >> 32));
   return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shr1_u64(uint64_t old, uint64_t v) {
+  const uint32_t lo = (uint32_t)dpp_shr1_i((int)(uint32_t)old, (int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)dpp_shr1_i((int)(uint32_t)(old >> 32), (int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
 }
 template <class T>
 __device__ __forceinline__ constexpr T id_none() {
@@ -235,13 +244,8 @@ struct WaveTopK {
         const float ud = shr1_f(cdd, d[r]);
         const T ui = id_shr1(cii, id[r]);
         const int idx = r * 64 + lane;
-        if (idx > pos) {
-          d[r] = ud;
-          id[r] = ui;
-        } else if (idx == pos) {
-          d[r] = vd;
-          id[r] = vi;
-        }
+        d[r] = idx > pos ? ud : (idx == pos ? vd : d[r]);
+        id[r] = idx > pos ? ui : (idx == pos ? vi : id[r]);
       }
       refresh_tau();
     }
@@ -256,13 +260,12 @@ template <int KK, int J, class T>
 __device__ __forceinline__ void bitonic_step(float& cd, T& ci, int lane) {
   const float od = xor_f<J>(cd);
   const T oi = id_xor<J>(ci);
-  const bool up = (lane & KK) == 0;
-  const bool lower = (lane & J) == 0;
-  const bool take = (lower == up) ? lexless(od, oi, cd, ci) : lexless(cd, ci, od, oi);
-  if (take) {
-    cd = od;
-    ci = oi;
-  }
+  const bool want_min = ((lane & J) == 0) == ((lane & KK) == 0);
+  const bool o_lt = lexless(od, oi, cd, ci);
+  const bool c_lt = lexless(cd, ci, od, oi);
+  const bool take = (want_min & o_lt) | (!want_min & c_lt);
+  cd = take ? od : cd;
+  ci = take ? oi : ci;
 }
 template <int KK, int J, class T>
 __device__ __forceinline__ void bitonic_steps(float& cd, T& ci, int lane) {
@@ -284,9 +287,10 @@ __device__ __forceinline__ void bulk_merge_row(WaveTopK<1, T>& tk, float cd, T c
   bitonic_sort64<2>(cd, ci, lane);
   const float rd = rev64_f(cd);
   const T ri = id_rev64(ci);
-  if (lexless(rd, ri, tk.d[0], tk.id[0])) {
-    tk.d[0] = rd;
-    tk.id[0] = ri;
+  {
+    const bool t = lexless(rd, ri, tk.d[0], tk.id[0]);
+    tk.d[0] = t ? rd : tk.d[0];
+    tk.id[0] = t ? ri : tk.id[0];
   }
   // ascending bitonic merge: KK = 128 keeps every lane "up"
   bitonic_steps<128, 32>(tk.d[0], tk.id[0], lane);
@@ -311,15 +315,14 @@ __device__ __forceinline__ void row16_merge(WaveTopK<1, T>& tk, float cd, T ci, 
   } else {
     ri = (T)rev16_i((int)ci);
   }
-  if (lexless(rd, ri, tk.d[0], tk.id[0])) {
-    tk.d[0] = rd;
-    tk.id[0] = ri;
+  {
+    const bool t = lexless(rd, ri, tk.d[0], tk.id[0]);
+    tk.d[0] = t ? rd : tk.d[0];
+    tk.id[0] = t ? ri : tk.id[0];
   }
   bitonic_steps<128, 8>(tk.d[0], tk.id[0], lane);
-  if (lane >= 16) {
-    tk.d[0] = kInf;
-    tk.id[0] = id_none<T>();
-  }
+  tk.d[0] = lane >= 16 ? kInf : tk.d[0];
+  tk.id[0] = lane >= 16 ? id_none<T>() : tk.id[0];
   tk.refresh_tau();
 }
 
@@ -330,14 +333,13 @@ __device__ __forceinline__ void row16_merge(WaveTopK<1, T>& tk, float cd, T ci, 
 // per-candidate serial insertion.
 template <int KL>
 __device__ __forceinline__ void cas_asc(float (&d)[KL], int64_t (&id)[KL], int a, int b) {
-  if (lexless(d[b], id[b], d[a], id[a])) {
-    const float td = d[a];
-    const int64_t ti = id[a];
-    d[a] = d[b];
-    id[a] = id[b];
-    d[b] = td;
-    id[b] = ti;
-  }
+  const bool t = lexless(d[b], id[b], d[a], id[a]);
+  const float da = d[a], db = d[b];
+  const int64_t ia = id[a], ib = id[b];
+  d[a] = t ? db : da;
+  id[a] = t ? ib : ia;
+  d[b] = t ? da : db;
+  id[b] = t ? ia : ib;
 }
 
 // in-register bitonic sort of KL (power of two) entries, ascending
@@ -365,10 +367,9 @@ template <int J>
 __device__ __forceinline__ void min_step(float& d, int64_t& id) {
   const float od = xor_f<J>(d);
   const int64_t oi = id_xor<J>(id);
-  if (lexless(od, oi, d, id)) {
-    d = od;
-    id = oi;
-  }
+  const bool t = lexless(od, oi, d, id);
+  d = t ? od : d;
+  id = t ? oi : id;
 }
 
 // lanes' lists sorted ascending -> the k smallest into (out_d, out_id) of lanes 0..k-1
@@ -594,8 +595,9 @@ __global__ __launch_bounds__(256) void k_select_rows(const float* __restrict__ d
 
 // ------------------------------------------------- coarse probe (MFMA path)
 // (key, column) packed so that unsigned 64-bit order is (key asc, column asc).
+// (-0 is folded into +0 first: the float order has them equal)
 __device__ __forceinline__ uint64_t pack_kc(float key, int col) {
-  return ((uint64_t)((uint32_t)f2ord(key) ^ 0x80000000u) << 32) | (uint32_t)col;
+  return ((uint64_t)((uint32_t)f2ord(key + 0.0f) ^ 0x80000000u) << 32) | (uint32_t)col;
 }
 __device__ __forceinline__ float kc_key(uint64_t p) { return ord2f((int)((uint32_t)(p >> 32) ^ 0x80000000u)); }
 constexpr uint64_t kKcNone = ~0ull;
@@ -1284,6 +1286,71 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const in
 }
 
 // ===================================================== list scan (phase B)
+// The scan's per-wave running top-k on packed (key, position) words
+// (pack_kc: unsigned 64-bit order == (key asc, position asc)): one 64-bit
+// compare and two selects per network step instead of float + id compares.
+template <int R>
+struct PackedTopK {
+  uint64_t p[R];  // sorted ascending across R rows x 64 lanes
+  uint64_t tp;    // the k-th best word (admission threshold), wave-uniform
+  int krow, klane;
+
+  __device__ __forceinline__ void init(int k) {
+#pragma unroll
+    for (int r = 0; r < R; r++) p[r] = kKcNone;
+    tp = kKcNone;
+    krow = (k - 1) >> 6;
+    klane = (k - 1) & 63;
+  }
+  __device__ __forceinline__ float td() const { return tp == kKcNone ? kInf : kc_key(tp); }
+  __device__ __forceinline__ void refresh_tau() {
+#pragma unroll
+    for (int r = 0; r < R; r++)
+      if (r == krow) tp = readlane_u64(p[r], klane);
+  }
+  // insert the candidate words c of the lanes set in `mask` (wave-uniform)
+  __device__ __forceinline__ void insert(uint64_t mask, uint64_t c, int lane) {
+    while (mask) {
+      const int src = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const uint64_t v = readlane_u64(c, src);
+      if (!(v < tp)) continue;  // overtaken by an earlier insert
+      int pos = 0;
+#pragma unroll
+      for (int r = 0; r < R; r++) pos += __popcll(__builtin_amdgcn_ballot_w64(p[r] < v));
+#pragma unroll
+      for (int r = R - 1; r >= 0; r--) {
+        if ((r + 1) * 64 <= pos) continue;  // row entirely before the slot
+        const uint64_t carry = r > 0 ? readlane_u64(p[r - 1], 63) : v;
+        const uint64_t u = shr1_u64(carry, p[r]);
+        const int idx = r * 64 + lane;
+        p[r] = idx > pos ? u : (idx == pos ? v : p[r]);
+      }
+      refresh_tau();
+    }
+  }
+};
+// merge up to 64 candidate words (one per lane, kKcNone = none) into a one-row top-k
+__device__ __forceinline__ void kc_bulk_merge(PackedTopK<1>& tk, uint64_t c, int lane) {
+  kc_sort64(c, lane);
+  kc_merge64(tk.p[0], c, lane);
+  tk.refresh_tau();
+}
+// up to 16 candidate words in lanes 0..15 into a one-row top-k with k <= 16:
+// 16-lane sort (DPP only), reverse-min against lanes 0..15, 16-lane merge
+__device__ __forceinline__ void kc_row16_merge(PackedTopK<1>& tk, uint64_t c, int lane) {
+  kc_steps<2, 1>(c, lane);
+  kc_steps<4, 2>(c, lane);
+  kc_steps<8, 4>(c, lane);
+  kc_steps<128, 8>(c, lane);  // every row ascending
+  const uint64_t rv = ((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(c >> 32)) << 32) | (uint32_t)rev16_i((int)(uint32_t)c);
+  uint64_t q = rv < tk.p[0] ? rv : tk.p[0];
+  kc_steps<128, 8>(q, lane);
+  tk.p[0] = lane >= 16 ? kKcNone : q;
+  tk.refresh_tau();
+}
+
+
 template <int G>
 struct LutVec;
 template <>
@@ -1528,7 +1595,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       loose = loose || bound[g] == kInf;
     }
 
-    WaveTopK<R, int> tk[G];
+    PackedTopK<R> tk[G];
 #pragma unroll
     for (int g = 0; g < G; g++) tk[g].init(k);
     int qn[G];  // this wave's queue fills (wave-uniform)
@@ -1558,9 +1625,8 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         for (int g = 0; g < G; g++) {
           if (b0 >= qn[g]) continue;
           const int e = b0 + lane;
-          const float cdg = e < qn[g] ? qd[wave][g * QG + e] : kInf;
-          const int cpg = e < qn[g] ? qi[wave][g * QG + e] : id_none<int>();
-          const bool p = lexless(cdg, cpg, tk[g].td, tk[g].ti);
+          const uint64_t cw64 = e < qn[g] ? pack_kc(qd[wave][g * QG + e], qi[wave][g * QG + e]) : kKcNone;
+          const bool p = cw64 < tk[g].tp;
           const uint64_t mk = __ballot(p);
           if (!mk) continue;
 #ifdef DIAG_DRAINCNT
@@ -1568,20 +1634,20 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #endif
           if constexpr (R == 1) {
             if (k <= 16 && qn[g] - b0 <= 16 && __popcll(mk) > 1)
-              row16_merge(tk[g], p ? cdg : kInf, p ? cpg : id_none<int>(), lane);
-            else if (__popcll(mk) > 6)
-              bulk_merge_row(tk[g], p ? cdg : kInf, p ? cpg : id_none<int>(), lane);
+              kc_row16_merge(tk[g], p ? cw64 : kKcNone, lane);
+            else if (__popcll(mk) > 4)
+              kc_bulk_merge(tk[g], p ? cw64 : kKcNone, lane);
             else
-              tk[g].insert(mk, cdg, cpg, lane);
+              tk[g].insert(mk, cw64, lane);
           } else {
-            tk[g].insert(mk, cdg, cpg, lane);
+            tk[g].insert(mk, cw64, lane);
           }
 #ifdef DIAG_DRAINCNT
-          asm volatile("" ::"v"(tk[g].d[0]), "s"(tk[g].td));
+          asm volatile("" ::"v"(tk[g].p[0]), "s"(tk[g].tp));
           const uint64_t tb1 = __builtin_amdgcn_s_memtime() - tb0;
           if (__popcll(mk) > 1) nbulk += tb1; else ninsert += tb1;
 #endif
-          bound[g] = fminf(bound[g], tk[g].td);
+          bound[g] = fminf(bound[g], tk[g].td());
         }
       }
 #pragma unroll
@@ -1590,9 +1656,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
       for (int g = 0; g < G; g++) {
         loose = loose || bound[g] == kInf;
-        if (g < ci.cnt && tk[g].td < kInf && lane == 0) {
-          atomicMin(&s_wb[g], f2ord(tk[g].td));
-          atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td));
+        if (g < ci.cnt && tk[g].tp != kKcNone && lane == 0) {
+          atomicMin(&s_wb[g], f2ord(tk[g].td()));
+          atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td()));
         }
       }
     };
@@ -1788,9 +1854,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       for (int r = 0; r < R; r++) {
         const int ix = r * 64 + lane;
         if (ix < k) {
-          const bool empty = tk[g].id[r] == id_none<int>();
-          pl.partD[o + ix] = empty ? FLT_MAX : tk[g].d[r];
-          pl.partI[o + ix] = empty ? -1 : ci.beg + tk[g].id[r];  // global code position
+          const bool empty = tk[g].p[r] == kKcNone;
+          pl.partD[o + ix] = empty ? FLT_MAX : kc_key(tk[g].p[r]);
+          pl.partI[o + ix] = empty ? -1 : ci.beg + (int64_t)(uint32_t)tk[g].p[r];  // global code position
         }
       }
     }
