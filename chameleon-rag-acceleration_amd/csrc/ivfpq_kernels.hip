@@ -646,33 +646,9 @@ __device__ __forceinline__ void kc_merge64(uint64_t& run, uint64_t p, int lane) 
 // Workgroup = 16 queries x 256 centroids (wave w: 4 tiles of 16 centroids).
 // Workgroups past the key tiles build T3 [nq][M][256] (Faiss tree order) for
 // 16 queries x 1024 entries each, when T3out is set.
-constexpr int GQ = 16, GC = 256, GE = 1024;
+constexpr int GQ = 16, GC = 128;
 
-// rows q0..q0+15 of x into xs[16][d] (zeros past nq); all loads before the stores
-__device__ __forceinline__ void fill_rows(float* xs, const float* __restrict__ x, int64_t q0, int64_t nq, int d,
-                                          int tid) {
-  const int64_t n = (int64_t)min<int64_t>(GQ, nq - q0) * d;
-  if ((d & 3) == 0) {
-    const float4* src = reinterpret_cast<const float4*>(x + q0 * d);
-    float4* dst = reinterpret_cast<float4*>(xs);
-    const int n4 = GQ * d / 4;
-    constexpr int U = 4;
-    for (int e0 = tid; e0 < n4; e0 += 256 * U) {
-      float4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int e = e0 + u * 256;
-        v[u] = 4 * (int64_t)e < n ? src[e] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        if (e0 + u * 256 < n4) dst[e0 + u * 256] = v[u];
-    }
-  } else {
-    for (int e = tid; e < GQ * d; e += 256) xs[e] = e < n ? x[q0 * d + e] : 0.f;
-  }
-}
-// the same rows transposed into xs[dk][16] (k-major; zeros past nq and d)
+// rows q0..q0+15 of x transposed into xs[dk][16] (k-major; zeros past nq and d)
 __device__ __forceinline__ void fill_cols(float* xs, const float* __restrict__ x, int64_t q0, int64_t nq, int d,
                                           int dk, int tid) {
   if ((d & 3) == 0 && d <= 1024) {
@@ -723,67 +699,38 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   if ((int)blockIdx.x < ngemm) return;
 #endif
   if ((int)blockIdx.x >= ngemm) {
-    // ---- T3 role: 16 queries x 1024 entries
+    // ---- T3 role: 16 queries x one sub-quantizer (256 entries, one per thread)
     const int tb = blockIdx.x - ngemm;
     const int total = t3.M * 256;
-    const int ne = (total + GE - 1) / GE;
-    const int64_t q0 = (int64_t)(tb / ne) * GQ;
-    const int e0 = (tb % ne) * GE;
-    float* xs = g_lds;  // [GQ][d]
-    fill_rows(xs, x, q0, nq, d, tid);
+    const int dsub = d / t3.M;
+    const int64_t q0 = (int64_t)(tb / t3.M) * GQ;
+    const int m = tb % t3.M;
+    const int e = m * 256 + tid;
+    float* xs = g_lds;  // [GQ][dsub]: the queries' sub-vectors m
+    for (int i = tid; i < GQ * dsub; i += 256) {
+      const int qq = i / dsub;
+      xs[i] = q0 + qq < nq ? x[(q0 + qq) * d + m * dsub + (i - qq * dsub)] : 0.f;
+    }
     __syncthreads();
     CDIAG(1);
-    const int dsub = d / t3.M;
     const int nqq = (int)min<int64_t>(GQ, nq - q0);
     if (dsub == 8) {
-      float4 cw[4][2];
+      const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
+      const float4 c0 = src[0], c1 = src[1];
+      const float w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int e = min(e0 + u * 256 + tid, total - 1);
-        const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
-        cw[u][0] = src[0];
-        cw[u][1] = src[1];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int e = e0 + u * 256 + tid;
-        if (e >= total) break;
-        const float* w = reinterpret_cast<const float*>(cw[u]);
-        const float* xm = xs + (e >> 8) * 8;
-        // 4 queries at a time: their sub-vectors are read before any tree
-        for (int g0 = 0; g0 < nqq; g0 += 4) {
-          float4 xv[4][2];
-#pragma unroll
-          for (int h = 0; h < 4; h++) {
-            const float4* src = reinterpret_cast<const float4*>(xm + min(g0 + h, GQ - 1) * d);
-            xv[h][0] = src[0];
-            xv[h][1] = src[1];
-          }
-#pragma unroll
-          for (int h = 0; h < 4; h++) {
-            if (g0 + h >= nqq) break;
-            const float* xq = reinterpret_cast<const float*>(xv[h]);
-#ifdef DIAG_G_NOSTORE
-            const float tv = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
-            asm volatile("" ::"v"(tv));
-#else
-            t3.out[(q0 + g0 + h) * total + e] =
-                tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
-#endif
-          }
-        }
+      for (int qq = 0; qq < GQ; qq++) {
+        const float4* xv = reinterpret_cast<const float4*>(xs + qq * 8);
+        const float4 x0 = xv[0], x1 = xv[1];
+        const float xq[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const float v = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
+        if (qq < nqq) t3.out[(q0 + qq) * total + e] = v;
       }
     } else {
-      for (int u = 0; u < 4; u++) {
-        const int e = e0 + u * 256 + tid;
-        if (e >= total) break;
-        const float* xm = xs + (e >> 8) * dsub;
-        const float* cwp = t3.cb + (int64_t)e * dsub;
-        for (int qq = 0; qq < nqq; qq++) {
-          const float* xq = xm + qq * d;
-          t3.out[(q0 + qq) * total + e] =
-              tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
-        }
+      const float* cwp = t3.cb + (int64_t)e * dsub;
+      for (int qq = 0; qq < nqq; qq++) {
+        const float* xq = xs + qq * dsub;
+        t3.out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
       }
     }
 #ifdef DIAG_CSTAMPS
@@ -792,10 +739,10 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     CDIAG(5);
     return;
   }
-  // ---- key tile: 16 queries x 256 centroids
+  // ---- key tile: 16 queries x 128 centroids
   const int nct = (nlist + GC - 1) / GC;
   const int64_t q0 = (int64_t)(blockIdx.x / nct) * GQ;
-  const int c0 = (blockIdx.x % nct) * GC + wave * 64;
+  const int c0 = (blockIdx.x % nct) * GC + wave * 32;
   const int dk = (d + 63) & ~63;  // A rows, zero-padded to whole double chunks
   float* xs = g_lds;              // [dk][GQ]: the A operand, k-major
   float* xn = xs + dk * GQ;       // [GQ]
@@ -826,32 +773,33 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     xn[tid] = tree<K_NORM>([&](int t) { return xs[t * GQ + tid]; }, [&](int t) { return xs[t * GQ + tid]; }, d);
   }
   typedef float f4 __attribute__((ext_vector_type(4)));
-  f4 acc[4];
+  constexpr int NTL = GC / 64;  // 16 x 16 tiles per wave
+  f4 acc[NTL];
 #pragma unroll
-  for (int t = 0; t < 4; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < NTL; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
   const int i16 = lane & 15, k4 = lane >> 4;
-  const float* bcol[4];
+  const float* bcol[NTL];
 #pragma unroll
-  for (int t = 0; t < 4; t++) bcol[t] = centT + min(c0 + t * 16 + i16, nlist - 1);  // clamped columns
+  for (int t = 0; t < NTL; t++) bcol[t] = centT + min(c0 + t * 16 + i16, nlist - 1);  // clamped columns
   // B operand rows, 8 k-steps (32 k) per chunk, two chunks in flight.  Rows
   // past d are clamped to row d - 1: their A entries are 0 and fma(0, b, acc)
   // == acc for every finite b (acc is never -0).
   constexpr int KS = 8;
-  float b0[KS][4], b1[KS][4];
-  auto load_b = [&](int k0, float (&b)[KS][4]) __attribute__((always_inline)) {
+  float b0[KS][NTL], b1[KS][NTL];
+  auto load_b = [&](int k0, float (&b)[KS][NTL]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < KS; j++) {
       const int64_t kr = min(k0 + 4 * j + k4, d - 1);
 #pragma unroll
-      for (int t = 0; t < 4; t++) b[j][t] = bcol[t][kr * ldc];
+      for (int t = 0; t < NTL; t++) b[j][t] = bcol[t][kr * ldc];
     }
   };
-  auto mma = [&](int k0, const float (&b)[KS][4]) __attribute__((always_inline)) {
+  auto mma = [&](int k0, const float (&b)[KS][NTL]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < KS; j++) {
       const float av = xs[(k0 + 4 * j + k4) * GQ + i16];
 #pragma unroll
-      for (int t = 0; t < 4; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
+      for (int t = 0; t < NTL; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
     }
   };
   load_b(0, b0);
@@ -864,7 +812,7 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   CDIAG(2);
   __syncthreads();  // xn
 #pragma unroll
-  for (int t = 0; t < 4; t++) {
+  for (int t = 0; t < NTL; t++) {
     const int c = c0 + t * 16 + i16;
     if (c >= nlist) continue;
     const float cnv = ip ? 0.f : cn[c];
@@ -2074,7 +2022,7 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
     t3.out = T3out;
     t3.cb = cb;
     t3.M = M;
-    t3.nblk = (int)(nqb * nblocks((int64_t)M * 256, GE));
+    t3.nblk = (int)(nqb * (unsigned)M);
   }
   const size_t smem = sizeof(float) * std::max<size_t>((size_t)GQ * ((d + 63) & ~63) + GQ * 9, (size_t)GQ * d);
   if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device
