@@ -156,7 +156,7 @@ struct ivfpq_index {
   // scratch
   DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
   // list-major plan workspaces (ivfpq_kernels.h ListPlan)
-  DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_tau;
+  DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_tau, p_qmask;
   // Stream ordering of the per-handle workspaces: every device search records
   // `done` on its stream; the next search (on any stream) waits for it, and
   // anything that frees or rewrites device buffers synchronizes on it first.
@@ -196,6 +196,7 @@ struct ivfpq_index {
     p_D.ensure(sizeof(float) * nq * np * 4 * k);
     p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
     p_tau.ensure(sizeof(int32_t) * nq);
+    p_qmask.ensure(sizeof(uint64_t) * nq);
     pl.cnt = p_cnt.as<int32_t>();
     pl.bucket = p_bucket.as<int2>();
     pl.recs = p_recs.as<int32_t>();
@@ -203,6 +204,7 @@ struct ivfpq_index {
     pl.partD = p_D.as<float>();
     pl.partI = p_I.as<int64_t>();
     pl.tauq = p_tau.as<int32_t>();
+    pl.qmask = p_qmask.as<uint64_t>();
     return pl;
   }
 

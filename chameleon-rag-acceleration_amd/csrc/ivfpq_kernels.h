@@ -76,6 +76,7 @@ struct ListPlan {
   float* partD;      // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k (keys)
   int64_t* partI;    // same shape: global code positions (-1 = none)
   int32_t* tauq;     // [nq] running k-th key per query (order-preserving int of the float, atomicMin)
+  uint64_t* qmask;   // [nq] probes the scan covers (nprobe <= 64): bit p = pair (q, p) is scanned
   int grid;          // persistent list-scan workgroups (multiple of 8)
 };
 

@@ -913,7 +913,10 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
     const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
     const uint64_t um = __ballot(use);
     const int fp = um ? (int)__builtin_ctzll(um) : 64;
-    if (lane == 0) cp.pl.tauq[q] = f2ord(kInf);
+    if (lane == 0) {
+      cp.pl.tauq[q] = f2ord(kInf);
+      cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
+    }
     if (use) {
       float d0 = rd;
       if (ip) {
@@ -1053,6 +1056,7 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
     const uint64_t um = __ballot(use);
     const int fp = (!found && um) ? (int)__builtin_ctzll(um) : 64;
     found = found || um != 0;
+    if (p0 == 0 && lane == 0) pl.qmask[q] = um;  // (nprobe <= 64 only: the merge reads it then)
     if (use) {
       float d0;
       if (ip) {
@@ -1840,11 +1844,8 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     constexpr int U = 16;
     float d[U];
     const int p = min(lane >> 2, np - 1);
-    bool scanned = false;
-    if ((lane >> 2) < np) {
-      const int64_t l = a.probe_list[q * np + p];
-      scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
-    }
+    // the planner's mask of the probes the scan covered (empty or foreign lists are not)
+    const bool scanned = (lane >> 2) < np && ((pl.qmask[q] >> p) & 1);
     const int64_t base = ((q * np + p) * 4 + (lane & 3)) * k;
     // unconditional, clamped loads (no divergent branch around them); slots of
     // unscanned probes (empty or foreign lists, lanes past nprobe) were never
@@ -1903,8 +1904,13 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       pos[b] = -1;
       if (e < total) {
         const int p = e / per_probe;
-        const int64_t l = a.probe_list[q * np + p];
-        const bool scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
+        bool scanned;
+        if (np <= 64) {
+          scanned = (pl.qmask[q] >> p) & 1;
+        } else {
+          const int64_t l = a.probe_list[q * np + p];
+          scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
+        }
         if (scanned) {
           d[b] = pd[e];
           pos[b] = pi[e];
