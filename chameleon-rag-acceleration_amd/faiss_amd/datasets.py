@@ -18,6 +18,10 @@ import time
 import numpy as np
 
 
+# The .ivecs/.fvecs readers and `evaluate` below follow the Faiss benchmark
+# helpers (MIT licence) that the reference reuses in
+# Chameleon/Faiss_experiments/datasets.py:13-52; the recall definition is kept
+# identical on purpose so the bench's recall column means the same thing.
 def ivecs_read(fname):
     a = np.fromfile(fname, dtype="int32")
     d = a[0]
