@@ -39,6 +39,25 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def lib_sha256():
+    import hashlib
+
+    from faiss_amd import _lib
+
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -61,7 +80,10 @@ def parse():
     p.add_argument("--event-every", type=int, default=5,
                    help="record the list-scan HIP events on every N-th timed step")
     p.add_argument("--no-recall", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r01_scan_pmc.json"))
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r02_scan_pmc.json"),
+                   help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
+                        "the library loaded now")
+    p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
     return p.parse_args()
 
 
@@ -170,6 +192,29 @@ def main():
     torch.cuda.synchronize()
     ix.set_timing(False)
     stage_split = ix.get_timing()
+
+    # extra rates (rank 0 view, untimed by the contract): k = 100 (the reference's
+    # profiling K) on the device path, and the host-buffer search() (PCIe included)
+    extra = {}
+    if not args.no_extra and not shard:
+        n_ex = max(5, min(20, args.steps))
+        D100 = torch.empty((Bg, 100), dtype=torch.float32, device=dev)
+        I100 = torch.empty((Bg, 100), dtype=torch.int64, device=dev)
+        ix.search_device(xq_dev[0], 100, D100, I100)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(n_ex):
+            ix.search_device(xq_dev[s % args.nbatches], 100, D100, I100)
+        torch.cuda.synchronize()
+        extra["k100_queries_per_s"] = n_ex * Bg / (time.perf_counter() - t0)
+        xq_host = [np.ascontiguousarray(xq[b * Bg:(b + 1) * Bg]) for b in range(args.nbatches)]
+        ix.search(xq_host[0], k)
+        t0 = time.perf_counter()
+        for s in range(n_ex):
+            ix.search(xq_host[s % args.nbatches], k)
+        extra["host_search_queries_per_s"] = n_ex * Bg / (time.perf_counter() - t0)
+        extra["note"] = (f"{n_ex} batches each; k100 = search_device with k=100; host_search = search() on numpy "
+                         f"queries (H2D copy, search, D2H copy; synchronous)")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -231,9 +276,11 @@ def main():
             ox.ntotal = ix.ntotal
             ox.nprobe = args.nprobe
             ns = min(args.cpu_sample, nq_total)
-            # this process's share of the host: OMP_NUM_THREADS (16 on the GPU box) capped by affinity
-            threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or O.default_threads(),
-                          O.default_threads())
+            # this process's share of the host: the cores in its affinity set, capped by
+            # OMP_NUM_THREADS (the GPU box's per-GPU CPU share is 16 and its pool asks
+            # worker pools to stay within it)
+            affinity = len(os.sched_getaffinity(0))
+            threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity, affinity)
             ox.search(xq[:64], k, threads)  # warm
             rates, tc, Ic = [], 0.0, None
             while len(rates) < 5 or (tc < args.cpu_seconds and len(rates) < 200):  # bounded: ~cpu_seconds
@@ -247,20 +294,28 @@ def main():
                 Ig = np.concatenate([ix.search(xq[i0:i0 + B], k)[1] for i0 in range(0, ns, B)])
                 agree = float((Ig == Ic).mean())
             cpu_baseline = {"value": float(np.median(rates)), "unit": "queries/s", "cores": threads, "kind": "port",
+                            "cpu_model": cpu_model(), "cores_in_affinity": affinity,
                             "sample": f"{ns} of the same queries (batch {B}), k={k}, nprobe={args.nprobe}, same "
                                       f"trained index; oracle/ivfpq_oracle.c (Faiss-1.7.1 order, scalar C, "
                                       f"OpenMP over queries); median of {len(rates)} repetitions, {tc:.1f}s total",
                             "gpu_id_agreement": agree}
 
     traffic = None
+    traffic_src = "no counter file"
     config_key = f"nb{args.nb}-d{args.d}-IVF{args.nlist}-PQ{args.M}-np{args.nprobe}-k{k}-B{B}-w{world}-{args.mode}"
+    sha = lib_sha256()
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if pm.get("config_key") == config_key:
+            if pm.get("config_key") != config_key:
+                traffic_src = "counter file is for another config"
+            elif pm.get("lib_sha256") != sha:
+                traffic_src = "counter file is stale (measured on another build of libivfpq.so)"
+            else:
                 traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+                traffic_src = os.path.relpath(args.pmc_json, REPO)
+        except Exception as e:  # malformed file: report, never guess
+            traffic_src = f"unreadable counter file: {e}"
 
     if rank == 0:
         out = {
@@ -292,6 +347,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "lib_sha256": sha,
                 "kernel": kernel,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": avg_launch_ms,
@@ -303,6 +360,7 @@ def main():
             "stages_ms_per_step": {s: v[0] / max(v[1], 1) for s, v in stage_split.items()},
             "recall": recall,
             "cpu_baseline": cpu_baseline,
+            "extra": extra or None,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -297,6 +297,30 @@ __device__ __forceinline__ void bulk_merge_row(WaveTopK<1, T>& tk, float cd, T c
   tk.refresh_tau();
 }
 
+// The same into an R-row top-k: the sorted candidates cascade down the rows,
+// each row keeping the lower half of (row, carry) and passing the upper half on.
+template <int R, class T>
+__device__ __forceinline__ void bulk_merge_rows(WaveTopK<R, T>& tk, float cd, T ci, int lane) {
+  bitonic_sort64<2>(cd, ci, lane);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const float rd = rev64_f(cd);
+    const T ri = id_rev64(ci);
+    const bool t = lexless(rd, ri, tk.d[r], tk.id[r]);
+    const float lo_d = t ? rd : tk.d[r], hi_d = t ? tk.d[r] : rd;
+    const T lo_i = t ? ri : tk.id[r], hi_i = t ? tk.id[r] : ri;
+    tk.d[r] = lo_d;
+    tk.id[r] = lo_i;
+    bitonic_steps<128, 32>(tk.d[r], tk.id[r], lane);
+    if (r + 1 < R) {
+      cd = hi_d;
+      ci = hi_i;
+      bitonic_steps<128, 32>(cd, ci, lane);
+    }
+  }
+  tk.refresh_tau();
+}
+
 // Merge up to 16 candidates held in lanes 0..15 (others (inf, none)) into a
 // single-row top-k with k <= 16: a 16-lane bitonic sort (DPP moves only), the
 // reverse-min against lanes 0..15 of the row, a 16-lane bitonic merge.  Only
@@ -1283,6 +1307,23 @@ struct PackedTopK {
   }
 };
 // merge up to 64 candidate words (one per lane, kKcNone = none) into a one-row top-k
+template <int R>
+__device__ __forceinline__ void kc_bulk_merge_rows(PackedTopK<R>& tk, uint64_t c, int lane) {
+  kc_sort64(c, lane);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint64_t rv = ((uint64_t)(uint32_t)rev64_i((int)(uint32_t)(c >> 32)) << 32) | (uint32_t)rev64_i((int)(uint32_t)c);
+    const bool t = rv < tk.p[r];
+    const uint64_t lo = t ? rv : tk.p[r], hi = t ? tk.p[r] : rv;
+    tk.p[r] = lo;
+    kc_steps<128, 32>(tk.p[r], lane);
+    if (r + 1 < R) {
+      c = hi;
+      kc_steps<128, 32>(c, lane);
+    }
+  }
+  tk.refresh_tau();
+}
 __device__ __forceinline__ void kc_bulk_merge(PackedTopK<1>& tk, uint64_t c, int lane) {
   kc_sort64(c, lane);
   kc_merge64(tk.p[0], c, lane);
@@ -1592,7 +1633,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
             else
               tk[g].insert(mk, cw64, lane);
           } else {
-            tk[g].insert(mk, cw64, lane);
+            if (__popcll(mk) > 4)
+              kc_bulk_merge_rows(tk[g], p ? cw64 : kKcNone, lane);
+            else
+              tk[g].insert(mk, cw64, lane);
           }
 #ifdef DIAG_DRAINCNT
           asm volatile("" ::"v"(tk[g].p[0]), "s"(tk[g].tp));
@@ -1925,11 +1969,12 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       const bool pass = maybe && lexless(d[b], id, tk.td, tk.ti);
       const uint64_t mask = __ballot(pass);
       if (!mask) continue;
-      if constexpr (R == 1) {
-        if (__popcll(mask) > 6) {
+      if (__popcll(mask) > 6) {
+        if constexpr (R == 1)
           bulk_merge_row(tk, pass ? d[b] : kInf, pass ? id : kSentinelId, lane);
-          continue;
-        }
+        else
+          bulk_merge_rows(tk, pass ? d[b] : kInf, pass ? id : kSentinelId, lane);
+        continue;
       }
       tk.insert(mask, d[b], id, lane);
     }

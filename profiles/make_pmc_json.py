@@ -2,7 +2,8 @@
 (profiles/pmc_kernel.sh output dir), corrected as MI355X_MICROARCH.md §HBM prescribes:
 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads on gfx950 (doubled here);
 WRITE_SIZE is taken as is.  The FETCH_SIZE unit is checked against TCC_EA0_RDREQ_sum x 64 B
-rather than assumed.  Usage: make_pmc_json.py <pmc dir> <config_key> <out.json>"""
+rather than assumed.  Usage: make_pmc_json.py <pmc dir> <config_key> <out.json> [libivfpq.so]
+The library's sha256 is recorded: bench.py uses the bytes only for the same build."""
 import collections
 import csv
 import glob
@@ -17,7 +18,7 @@ def short(n):
     return n.split("(")[0].replace("chivf::", "")
 
 
-def main(d, key, out):
+def main(d, key, out, lib=None):
     agg = collections.defaultdict(list)
     for f in sorted(glob.glob(os.path.join(d, "g*", "run_counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -25,6 +26,10 @@ def main(d, key, out):
     mean = {kc: sum(v) / len(v) for kc, v in agg.items()}
     kernels = sorted({k for k, _ in mean})
     res = {"config_key": key, "source": os.path.relpath(d), "kernels": {}}
+    if lib:
+        import hashlib
+
+        res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()
     for k in kernels:
         f = mean.get((k, "FETCH_SIZE"))
         w = mean.get((k, "WRITE_SIZE"))
@@ -48,4 +53,4 @@ def main(d, key, out):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

@@ -10,15 +10,16 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT/pmc"
 cd /tmp && export TMPDIR=/tmp
-PB="$R/bench.py --no-recall --no-cpu-baseline --steps 10 --warmup 2 $*"
+PB="$R/bench.py --no-recall --no-cpu-baseline --no-extra --steps 10 --warmup 2 $*"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_scan|k_merge_probes|k_coarse|k_ip_table" \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "k_scan|k_merge_probes|k_coarse|k_plan" \
     --output-format csv -d "$OUT/pmc/g$i" -o run -- python3 $PB > "$OUT/pmc/g$i.json" 2> "$OUT/pmc/g$i.err" || exit $?
   i=$((i+1))
 done
 KEY=$(python3 -c "import json,sys; j=json.load(open('$OUT/pmc/g0.json')); c=j['config']; print(c['key'])")
-python3 $R/profiles/make_pmc_json.py "$OUT/pmc" "$KEY" "$OUT/scan_pmc.json" > /dev/null || exit $?
+LIB=$(python3 -c "import sys; sys.path.insert(0, '$R/chameleon-rag-acceleration_amd'); from faiss_amd import _lib; print(_lib.LIB_PATH)")
+python3 $R/profiles/make_pmc_json.py "$OUT/pmc" "$KEY" "$OUT/scan_pmc.json" "$LIB" > /dev/null || exit $?
 timeout -k 10 400 python3 $R/bench.py --pmc-json "$OUT/scan_pmc.json" "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 $R/bench.py --pmc-json "$OUT/scan_pmc.json" "$@" > "$OUT/bench_traced.json" 2> "$OUT/bench_traced.err" || exit $?
