@@ -10,8 +10,10 @@ already resident in HBM.
 
 N > 1 (one process per GPU, torch.distributed over RCCL): the index is sharded
 by inverted-list range; the global batch is 1024 x N queries (weak scaling: the
-code bytes each GPU scans per step stay constant), every rank scans its lists
-for the whole batch and an all_to_all returns each query slice's partials to
+code bytes each GPU scans per step stay constant).  Each rank runs the coarse
+quantizer on its own 1024-query slice, an all_gather shares the (list, dis0)
+probe arrays, every rank scans its lists for the whole batch
+(search_preassigned) and an all_to_all returns each query slice's partials to
 its owner, which merges them on the GPU.  ``--mode replicas`` instead runs N
 independent full replicas.
 
@@ -103,7 +105,7 @@ def main():
 
     import faiss_amd as faiss
     from faiss_amd import datasets
-    from faiss_amd.sharding import balanced_list_ranges, exchange_partials
+    from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials
 
     t_setup = time.time()
     shard = world > 1 and args.mode == "shard"
@@ -155,8 +157,11 @@ def main():
     merged = {}
 
     def step(b):
-        if shard:
-            Dp, Ip = ix.search_device(xq_dev[b], k, Dbuf, Ibuf)
+        if shard:  # coarse for this rank's slice, probes all-gathered, own lists scanned for the batch
+            xg = xq_dev[b]
+            Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
+            Dq, Iq = all_gather_probes(Dq_s, Iq_s, world)
+            Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbuf, Ibuf)
             Ds, Is = exchange_partials(Dp, Ip, world)
             merged[b] = faiss.merge_topk_device(Ds, Is)
         else:

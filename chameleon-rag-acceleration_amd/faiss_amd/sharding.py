@@ -10,8 +10,13 @@ One process per GPU (``torch.distributed``, backend ``nccl`` = RCCL on ROCm):
   ranges are contiguous and balanced by code bytes (lists are imbalanced,
   ``bench_polysemous_1bn.py:368``).
 * Every rank holds the global query batch (``world`` slices of ``B`` queries,
-  slice ``j`` owned by rank ``j``), computes the coarse probe for it, scans its
-  own lists and produces a partial sorted top-k per query.
+  slice ``j`` owned by rank ``j``).  Rank ``j`` runs the coarse quantizer for
+  its own slice only; one ``all_gather`` of the ``[B, nprobe]`` (list, dis0)
+  arrays (``B * nprobe * 12`` bytes per rank, ~200 KB at C2) gives every rank
+  the probes of the whole batch, and it scans its own lists for them
+  (``search_preassigned``: the same pairs and dis0 as an unsharded search, so
+  the result is bit-identical).  Per-rank coarse work stays flat in N; the T3
+  tables (61 kFLOP per query) are built for the whole batch.
 * One ``all_to_all`` sends slice ``j`` of every partial result to rank ``j``
   (``world * B * k * 12`` bytes per rank — latency-bound on xGMI), and each
   rank merges its ``world`` partial lists by (distance, label) on the GPU.
@@ -81,6 +86,26 @@ def exchange_partials(Dp, Ip, world, group=None):
     return Ds, Is
 
 
+def all_gather_probes(Dq, Iq, world, group=None):
+    """All-gather of the per-slice coarse results: [B, nprobe] -> [world * B, nprobe]."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return Dq, Iq
+    if dist.get_backend(group) == "gloo":
+        gD = [torch.empty_like(Dq) for _ in range(world)]
+        gI = [torch.empty_like(Iq) for _ in range(world)]
+        dist.all_gather(gD, Dq.contiguous(), group=group)
+        dist.all_gather(gI, Iq.contiguous(), group=group)
+        return torch.cat(gD), torch.cat(gI)
+    outD = torch.empty((world * Dq.shape[0], Dq.shape[1]), dtype=Dq.dtype, device=Dq.device)
+    outI = torch.empty((world * Iq.shape[0], Iq.shape[1]), dtype=Iq.dtype, device=Iq.device)
+    dist.all_gather_into_tensor(outD, Dq.contiguous(), group=group)
+    dist.all_gather_into_tensor(outI, Iq.contiguous(), group=group)
+    return outD, outI
+
+
 def merge_partials_reference(Ds, Is):
     """Host merge of [S, n, k] sorted partials by (distance, label); -1 labels last.
     Test reference for the device merge (faiss_amd.merge_topk_device)."""
@@ -102,18 +127,36 @@ def merge_partials_reference(Ds, Is):
 class ShardedSearch:
     """Per-rank driver of a list-range-sharded search.
 
-    ``local_search(xq_global, k) -> (Dp, Ip)`` runs this rank's shard (the GPU
-    engine in production); ``merge(Ds, Is) -> (D, I)`` merges the exchanged
+    With ``coarse(x_slice) -> (Dq, Iq)`` and ``local_preassigned(xq_global, k,
+    Iq, Dq) -> (Dp, Ip)`` (``IndexIVFPQ.coarse_device`` and
+    ``search_preassigned_device`` in production) the coarse quantizer runs on
+    this rank's query slice only and the probes are all-gathered; otherwise
+    ``local_search(xq_global, k)`` runs the whole search of the global batch on
+    this rank's lists.  ``merge(Ds, Is) -> (D, I)`` merges the exchanged
     partials (``faiss_amd.merge_topk_device`` in production).
     """
 
-    def __init__(self, local_search, merge, world, group=None):
+    def __init__(self, local_search, merge, world, group=None, coarse=None, local_preassigned=None):
         self.local_search = local_search
         self.merge = merge
         self.world = world
         self.group = group
+        self.coarse = coarse
+        self.local_preassigned = local_preassigned
+
+    def partials(self, xq_global, k):
+        """This rank's partial top-k [world * B, k] over its lists for the global batch."""
+        if self.coarse is None or self.local_preassigned is None:
+            return self.local_search(xq_global, k)
+        import torch.distributed as dist
+
+        rank = dist.get_rank(self.group) if self.world > 1 else 0
+        B = xq_global.shape[0] // self.world
+        Dq, Iq = self.coarse(xq_global[rank * B:(rank + 1) * B])
+        Dq, Iq = all_gather_probes(Dq, Iq, self.world, self.group)
+        return self.local_preassigned(xq_global, k, Iq, Dq)
 
     def search(self, xq_global, k):
-        Dp, Ip = self.local_search(xq_global, k)
+        Dp, Ip = self.partials(xq_global, k)
         Ds, Is = exchange_partials(Dp, Ip, self.world, self.group)
         return self.merge(Ds, Is)

@@ -44,7 +44,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, golden, out):
+def _worker(rank, world, port, golden, out, slice_coarse=False):
     import sys
 
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -78,8 +78,18 @@ def _worker(rank, world, port, golden, out):
         D, I = merge_partials_reference(Ds.numpy(), Is.numpy())
         return torch.from_numpy(D), torch.from_numpy(I)
 
+    def coarse(xs):  # this rank's query slice only
+        dis, lists = O.coarse_search(xs.numpy(), z["centroids"], ox.nprobe)
+        return torch.from_numpy(dis), torch.from_numpy(lists)
+
+    def local_pre(xq, kk, Iq, Dq):  # the gathered probes of the whole batch, this rank's lists
+        D, I = ox.search_preassigned(xq.numpy(), kk, Iq.numpy(), Dq.numpy())
+        return torch.from_numpy(D), torch.from_numpy(I)
+
     xq = torch.from_numpy(z["xq"])  # global batch: world slices
-    D, I = ShardedSearch(local, merge, world).search(xq, k)
+    ss = ShardedSearch(local, merge, world, coarse=coarse if slice_coarse else None,
+                       local_preassigned=local_pre if slice_coarse else None)
+    D, I = ss.search(xq, k)
     gD = [torch.empty_like(D) for _ in range(world)]
     gI = [torch.empty_like(I) for _ in range(world)]
     dist.all_gather(gD, D)
@@ -90,12 +100,15 @@ def _worker(rank, world, port, golden, out):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("slice_coarse", [False, True], ids=["global_coarse", "sliced_coarse_allgather"])
 @pytest.mark.parametrize("case", ["d128_m16", "d96_m8_dsub12"])
-def test_sharded_search_equals_unsharded(tmp_path, golden_dir, case):
+def test_sharded_search_equals_unsharded(tmp_path, golden_dir, case, slice_coarse):
+    """Both shard flows: every rank probing the whole batch, and each rank probing
+    its own query slice with the (list, dis0) arrays all-gathered."""
     world = 2
     golden = os.path.join(golden_dir, f"ivfpq_{case}.npz")
     out = str(tmp_path / "res.npz")
-    mp.spawn(_worker, args=(world, _free_port(), golden, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), golden, out, slice_coarse), nprocs=world, join=True)
     r = np.load(out)
     z = np.load(golden)
     np.testing.assert_array_equal(r["I"], z["or_I"])

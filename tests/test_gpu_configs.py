@@ -201,3 +201,47 @@ def test_c4_shape_m48_nlist65536(c4_shape, k):
     D, I = ix.search(xq, k)
     Dr, Ir = ox.search(xq, k)
     assert_same(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("nshards", [2, 4])
+def test_sliced_coarse_allgather_shards_c2(sift1m, nshards):
+    """bench.py's shard flow emulated on one GPU: rank r runs the coarse
+    quantizer on its own 1024/N-query slice only, the (list, dis0) arrays of all
+    slices are concatenated (the all_gather), every rank scans its list range
+    for the whole batch with search_preassigned_device, and each slice's N
+    partials are merged on the device (the all_to_all + merge).  Must equal the
+    unsharded oracle bit for bit."""
+    import torch
+
+    ix, ox, xq = sift1m
+    ox.nprobe = 16
+    ix.nprobe = 16
+    sizes = ix.invlists.list_sizes()
+    ranges = balanced_list_ranges(sizes, nshards, ix.M)
+    xd = torch.from_numpy(xq).cuda()
+    B = xd.shape[0] // nshards
+    shards = []
+    for lo, hi in ranges:
+        sh = faiss.IndexIVFPQ(None, ix.d, ix.nlist, ix.M, 8, device=0)
+        sh.set_trained(ix.centroids(), ix.codebook())
+        sh.set_list_range(lo, hi)
+        lists = [l for l in range(lo, hi) if sizes[l]]
+        sh.add_preencoded(np.concatenate([np.full(sizes[l], l, np.int64) for l in lists]),
+                          np.concatenate([ix.invlists.get_codes(l).reshape(-1, ix.M) for l in lists]),
+                          np.concatenate([ix.invlists.get_ids(l) for l in lists]))
+        sh.nprobe = 16
+        shards.append(sh)
+    probes = [shards[r].coarse_device(xd[r * B:(r + 1) * B]) for r in range(nshards)]
+    Dq = torch.cat([p[0] for p in probes])
+    Iq = torch.cat([p[1] for p in probes])
+    parts = [sh.search_preassigned_device(xd, 10, Iq, Dq) for sh in shards]
+    Dm, Im = [], []
+    for r in range(nshards):  # slice r's partials from every rank, merged
+        Ds = torch.stack([p[0][r * B:(r + 1) * B] for p in parts])
+        Is = torch.stack([p[1][r * B:(r + 1) * B] for p in parts])
+        D, I = faiss.merge_topk_device(Ds, Is)
+        Dm.append(D)
+        Im.append(I)
+    torch.cuda.synchronize()
+    Dr, Ir = ox.search(xq, 10)
+    assert_same(torch.cat(Dm).cpu().numpy(), torch.cat(Im).cpu().numpy(), Dr, Ir)
