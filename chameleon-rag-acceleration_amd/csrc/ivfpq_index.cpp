@@ -815,6 +815,16 @@ int ivfpq_merge_topk_device(int S, int64_t n, int k, int metric, const float* Di
   });
 }
 
+int ivfpq_linear_transform_device(int64_t n, int d_in, int d_out, const float* AT, const float* b, const float* x,
+                                  float* y, void* stream) {
+  return guarded([&] {
+    require(n >= 0 && d_in >= 1 && d_out >= 1, "invalid transform shape");
+    require(n == 0 || (AT && x && y), "null buffer");
+    launch_linear_transform(x, n, d_in, AT, b, d_out, y, (hipStream_t)stream);
+    HIPCHECK(hipGetLastError());
+  });
+}
+
 int ivfpq_set_timing(ivfpq_index* h, int on) {
   return guarded([&] {
     check_handle(h);

@@ -47,6 +47,10 @@ void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, 
                           hipStream_t s, bool ip, const ListPlan* plan = nullptr, const int64_t* list_off = nullptr,
                           int lo = 0, int hi = 0, const float* x = nullptr, const float* cent = nullptr, int d = 0);
 
+// y[i][j] = sum_t x[i][t] * AT[t][j] (t-ordered fmaf chain) + b[j] (b nullable): OPQ / LinearTransform apply
+void launch_linear_transform(const float* x, int64_t n, int d_in, const float* AT, const float* b, int d_out, float* y,
+                             hipStream_t s);
+
 // T3[q][m][j] = <x_q[m], C_mj>  (Faiss AVX order)
 void launch_ip_table(const float* x, int64_t n, int d, const float* codebook, int M, int ksub, float* out,
                      hipStream_t s);

@@ -957,6 +957,24 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
   SDIAG(5);
 }
 
+// ------------------------------------------------------ linear pre-transform
+// y[i][j] = sum_t x[i][t] * A[j][t] (+ b[j]), the OPQ / LinearTransform apply
+// (Faiss VectorTransform::apply, bench_gpu_1bn.py:485-489): a t-ordered fmaf
+// chain from 0 (the oracle's or_linear_transform order), bias added last.
+// AT = A transposed [d_in][d_out]: the threads of a row read it coalesced.
+__global__ __launch_bounds__(256) void k_linear_transform(const float* __restrict__ x, int64_t n, int d_in,
+                                                          const float* __restrict__ AT, const float* __restrict__ b,
+                                                          int d_out, float* __restrict__ y) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= n * d_out) return;
+  const int64_t i = gid / d_out;
+  const int j = (int)(gid - i * d_out);
+  const float* xi = x + i * d_in;
+  float acc = 0.f;
+  for (int t = 0; t < d_in; t++) acc = __builtin_fmaf(xi[t], AT[(int64_t)t * d_out + j], acc);
+  y[gid] = b ? acc + b[j] : acc;
+}
+
 // -------------------------------------------------------------- PQ tables
 // T3, one workgroup per query: thread t computes entries [16t, 16t+16) of the
 // query's M x 256 table (m = t / 16); q is staged in LDS, codebook rows are
@@ -2104,6 +2122,12 @@ void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, 
   }
   hipLaunchKernelGGL(k_coarse_select, dim3(nblocks(nq, 4)), dim3(256), 0, s, keys, nq, nlist, nprobe, out_dis,
                      out_list, ip ? 1 : 0, x, d, cp);
+}
+
+void launch_linear_transform(const float* x, int64_t n, int d_in, const float* AT, const float* b, int d_out, float* y,
+                             hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_linear_transform, dim3(nblocks(n * d_out, 256)), dim3(256), 0, s, x, n, d_in, AT, b, d_out, y);
 }
 
 void launch_ip_table(const float* x, int64_t n, int d, const float* cb, int M, int ksub, float* out,

@@ -14,6 +14,8 @@ from .index import (  # noqa: F401
     IndexFlatL2,
     IndexIVFPQ,
     ParameterSpace,
+    downcast_index,
+    extract_index_ivf,
     get_num_gpus,
     index_factory,
     merge_topk_device,
@@ -21,6 +23,14 @@ from .index import (  # noqa: F401
     swig_ptr,
     vector_to_array,
     write_index,
+)
+from .transform import (  # noqa: F401
+    IndexPreTransform,
+    LinearTransform,
+    OPQMatrix,
+    downcast_VectorTransform,
+    read_VectorTransform,
+    write_VectorTransform,
 )
 from . import contrib  # noqa: F401
 from .contrib import ivf_tools  # noqa: F401

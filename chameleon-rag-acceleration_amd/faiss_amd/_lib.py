@@ -50,6 +50,9 @@ SIGNATURES = {
     "ivfpq_merge_topk_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p]),
+    "ivfpq_linear_transform_device": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_void_p]),
     "ivfpq_set_timing": (ctypes.c_int, [c_handle, ctypes.c_int]),
     "ivfpq_get_timing": (ctypes.c_int, [c_handle, ctypes.POINTER(ctypes.c_double), c_i64p]),
     "ivfpq_ntotal": (ctypes.c_int64, [c_handle]),

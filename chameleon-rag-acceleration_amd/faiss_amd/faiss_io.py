@@ -22,6 +22,12 @@ The layout is restated from upstream Faiss 1.7.1 ``impl/index_write.cpp`` /
         "full" + u64 count + u64 sizes[nlist]   |   "sprs" + u64 count + u64 (list, size) pairs
         per non-empty list: codes u8[n * code_size], then ids i64[n]
 
+    "IxPT"                                   IndexPreTransform (the OPQ front of "OPQ16,IVF..,PQ16")
+      index header (d = the chain's d_in), nt i32, nt x VectorTransform, then the wrapped index
+      VectorTransform "LTra" (LinearTransform, and OPQMatrix, which Faiss writes as a plain
+      LinearTransform): have_bias u8, A = u64 count + f32[d_out * d_in], b = u64 count + f32[count],
+      d_in i32, d_out i32, is_trained u8
+
 Parity is unpinned: no Faiss-written file exists in the reference or this image
 (the reference's ``*.index`` files are not shipped), so the tests check a
 hand-assembled byte layout and round trips, not a file from real Faiss.
@@ -37,9 +43,13 @@ FOURCC_FLAT = {0: b"IxFI", 1: b"IxF2"}  # metric_type: 0 = INNER_PRODUCT, 1 = L2
 HEADER_DUMMY = 1 << 20
 
 
+FOURCC_PRETRANSFORM = b"IxPT"
+FOURCC_LINEAR = b"LTra"
+
+
 def is_faiss_file(path) -> bool:
     with open(path, "rb") as f:
-        return f.read(4) in (FOURCC_IVFPQ, b"IvPQ")
+        return f.read(4) in (FOURCC_IVFPQ, b"IvPQ", FOURCC_PRETRANSFORM)
 
 
 class _Reader:
@@ -81,7 +91,71 @@ def parse_ivfpq(buf: bytes) -> dict:
     """Faiss IndexIVFPQ bytes -> {d, nlist, nprobe, M, nbits, metric, is_trained,
     centroids [nlist][d], codebook [M][ksub][dsub], lists: [(ids i64[n], codes u8[n][code_size])]}."""
     r = _Reader(buf)
+    z = _parse_ivfpq(r, r.fourcc())
+    if r.o != len(r.b):
+        raise RuntimeError("trailing bytes after the index")
+    return z
+
+
+def parse_index(buf: bytes) -> dict:
+    """IndexIVFPQ or IndexPreTransform(LinearTransform..., IndexIVFPQ) bytes.
+    IVF-PQ -> parse_ivfpq's dict with kind "ivfpq"; pre-transform -> {kind
+    "pretransform", d, ntotal, metric, chain: [{A [d_out][d_in], b, have_bias,
+    d_in, d_out, is_trained}], index: the IVF-PQ dict}."""
+    r = _Reader(buf)
     h = r.fourcc()
+    if h == FOURCC_PRETRANSFORM:
+        d, ntotal, is_trained, metric = r.header()
+        nt = r.fmt("i")
+        chain = [_parse_linear(r) for _ in range(nt)]
+        if not chain or chain[0]["d_in"] != d:
+            raise RuntimeError("pre-transform chain does not match the index dimension")
+        sub = _parse_ivfpq(r, r.fourcc())
+        if sub["d"] != chain[-1]["d_out"]:
+            raise RuntimeError("pre-transform output dimension does not match the wrapped index")
+        z = {"kind": "pretransform", "d": d, "ntotal": ntotal, "metric": metric, "chain": chain, "index": sub}
+    else:
+        z = _parse_ivfpq(r, h)
+    if r.o != len(r.b):
+        raise RuntimeError("trailing bytes after the index")
+    return z
+
+
+def _parse_linear(r: _Reader) -> dict:
+    vh = r.fourcc()
+    if vh != FOURCC_LINEAR:
+        raise RuntimeError(f"unsupported VectorTransform {vh!r} (LinearTransform / OPQMatrix only)")
+    have_bias = r.fmt("B") != 0
+    A = r.vector(np.float32)
+    b = r.vector(np.float32)
+    d_in = r.fmt("i")
+    d_out = r.fmt("i")
+    t_trained = r.fmt("B") != 0
+    if t_trained and A.size != d_in * d_out:
+        raise RuntimeError("LinearTransform matrix has the wrong size")
+    if have_bias and t_trained and b.size != d_out:
+        raise RuntimeError("LinearTransform bias has the wrong size")
+    return {"A": A.reshape(d_out, d_in) if A.size else A, "b": b if have_bias else None,
+            "have_bias": have_bias, "d_in": d_in, "d_out": d_out, "is_trained": t_trained}
+
+
+def parse_vector_transform(buf: bytes) -> dict:
+    """A faiss.write_VectorTransform file (bench_gpu_1bn.py:507-510): one "LTra" record."""
+    r = _Reader(buf)
+    t = _parse_linear(r)
+    if r.o != len(r.b):
+        raise RuntimeError("trailing bytes after the VectorTransform")
+    return t
+
+
+def serialize_linear(A, b, d_in, d_out, is_trained=True) -> bytes:
+    A = np.zeros(0, np.float32) if A is None else np.ascontiguousarray(A, np.float32).reshape(-1)
+    bb = np.zeros(0, np.float32) if b is None else np.ascontiguousarray(b, np.float32).reshape(-1)
+    return b"".join([FOURCC_LINEAR, struct.pack("<B", 0 if b is None else 1), _vector(A), _vector(bb),
+                     struct.pack("<iiB", d_in, d_out, 1 if is_trained else 0)])
+
+
+def _parse_ivfpq(r: _Reader, h: bytes) -> dict:
     if h == b"IvPQ":
         raise RuntimeError("legacy IvPQ Faiss files (pre-1.5 inverted lists) are not supported")
     if h != FOURCC_IVFPQ:
@@ -139,7 +213,7 @@ def parse_ivfpq(buf: bytes) -> dict:
         lists.append((ids, codes))
     if int(sizes.sum()) != ntotal:
         raise RuntimeError("inverted list sizes do not add up to ntotal")
-    return {"d": d, "nlist": nlist, "nprobe": nprobe, "M": M, "nbits": nbits, "metric": metric,
+    return {"kind": "ivfpq", "d": d, "nlist": nlist, "nprobe": nprobe, "M": M, "nbits": nbits, "metric": metric,
             "is_trained": is_trained, "centroids": xb.reshape(nlist, d) if xb.size else xb,
             "codebook": cb.reshape(M, 256, d // M) if cb.size else cb, "lists": lists}
 
@@ -175,4 +249,13 @@ def serialize_ivfpq(d, nlist, nprobe, M, nbits, metric, centroids, codebook, lis
         if len(ids):
             out.append(np.ascontiguousarray(codes, np.uint8).tobytes())
             out.append(np.ascontiguousarray(ids, np.int64).tobytes())
+    return b"".join(out)
+
+
+def serialize_pretransform(d, metric, chain, sub: bytes, ntotal, is_trained=True) -> bytes:
+    """IndexPreTransform bytes: chain = [(A [d_out][d_in] | None, b | None, d_in, d_out, is_trained)],
+    sub = the wrapped index's bytes (serialize_ivfpq)."""
+    out = [FOURCC_PRETRANSFORM, _header(d, ntotal, is_trained, metric), struct.pack("<i", len(chain))]
+    out += [serialize_linear(*t) for t in chain]
+    out.append(sub)
     return b"".join(out)

@@ -55,6 +55,16 @@ def vector_to_array(v):
     return np.asarray(v).copy()
 
 
+def downcast_index(index):
+    """faiss.downcast_index: Python objects already have their concrete type."""
+    return index
+
+
+def extract_index_ivf(index):
+    """faiss.extract_index_ivf: the IndexIVFPQ inside an IndexPreTransform."""
+    return getattr(index, "index", index)
+
+
 def get_num_gpus():
     return int(_lib.load().ivfpq_device_count())
 
@@ -497,21 +507,35 @@ def merge_topk_device(Ds, Is, metric=METRIC_L2, stream=None):
 
 # ------------------------------------------------------------------ factory / IO
 
-_FACTORY_RE = re.compile(r"^IVF(\d+),PQ(\d+)(?:x(\d+))?$")
+_FACTORY_RE = re.compile(r"^(?:OPQ(\d+)(?:_(\d+))?,)?IVF(\d+),PQ(\d+)(?:x(\d+))?$")
 
 
 def parse_factory(key):
+    """'[OPQ<M>[_<dout>],]IVF<nlist>,PQ<M>[x8]' -> (nlist, M, nbits) or, with an
+    OPQ front, (nlist, M, nbits, opq_M, opq_dout) (opq_dout = -1: d)."""
     m = _FACTORY_RE.match(key.replace(" ", ""))
     if not m:
-        raise RuntimeError(f"index_factory: unsupported key {key!r} (supported: 'IVF<nlist>,PQ<M>[x8]')")
-    nbits = int(m.group(3)) if m.group(3) else 8
-    return int(m.group(1)), int(m.group(2)), nbits
+        raise RuntimeError(f"index_factory: unsupported key {key!r} "
+                           "(supported: '[OPQ<M>[_<dout>],]IVF<nlist>,PQ<M>[x8]')")
+    nbits = int(m.group(5)) if m.group(5) else 8
+    base = (int(m.group(3)), int(m.group(4)), nbits)
+    if m.group(1) is None:
+        return base
+    return base + (int(m.group(1)), int(m.group(2)) if m.group(2) else -1)
 
 
 def index_factory(d, key, metric=METRIC_L2, device=None):
-    """faiss.index_factory(d, "IVF1024,PQ16") (bench_polysemous_1bn.py:272)."""
-    nlist, M, nbits = parse_factory(key)
-    return IndexIVFPQ(None, d, nlist, M, nbits, metric, device)
+    """faiss.index_factory(d, "IVF1024,PQ16") (bench_polysemous_1bn.py:272) and the
+    OPQ-fronted "OPQ16,IVF262144,PQ16" (bench_gpu_1bn.py:10-17)."""
+    from .transform import IndexPreTransform, OPQMatrix
+
+    f = parse_factory(key)
+    if len(f) == 3:
+        nlist, M, nbits = f
+        return IndexIVFPQ(None, d, nlist, M, nbits, metric, device)
+    nlist, M, nbits, opq_M, opq_dout = f
+    opq = OPQMatrix(d, opq_M, opq_dout)
+    return IndexPreTransform(opq, IndexIVFPQ(None, opq.d_out, nlist, M, nbits, metric, device))
 
 
 class ParameterSpace:
@@ -533,39 +557,61 @@ class ParameterSpace:
             self.set_index_parameter(index, name.strip(), float(value))
 
 
-def write_index(index, path, fmt="faiss"):
-    """Persist ``index``.  fmt "faiss": the Faiss 1.7.1 IndexIVFPQ binary layout
-    (``faiss.read_index`` loads it; faiss_io.py); "native": this library's CHIVFPQ1
-    image (also keeps untrained indexes)."""
-    if fmt == "native" or not index.is_trained:
-        _lib.check(_lib.load().ivfpq_save(index._h, str(path).encode()))
-        return
-    if fmt != "faiss":
-        raise RuntimeError(f"unknown index file format {fmt!r}")
+def _ivfpq_bytes(index):
     inv = index.invlists
     lists = [(inv.get_ids(l), inv.get_codes(l).reshape(-1, index.code_size)) for l in range(index.nlist)]
-    buf = faiss_io.serialize_ivfpq(index.d, index.nlist, index.nprobe, index.M, index.nbits, index.metric_type,
-                                   index.centroids(), index.codebook(), lists)
+    return faiss_io.serialize_ivfpq(index.d, index.nlist, index.nprobe, index.M, index.nbits, index.metric_type,
+                                    index.centroids(), index.codebook(), lists)
+
+
+def write_index(index, path, fmt="faiss"):
+    """Persist ``index``.  fmt "faiss": the Faiss 1.7.1 IndexIVFPQ / IndexPreTransform
+    binary layout (``faiss.read_index`` loads it; faiss_io.py); "native": this
+    library's CHIVFPQ1 image (also keeps untrained indexes; IVF-PQ only)."""
+    from .transform import IndexPreTransform
+
+    if isinstance(index, IndexPreTransform):
+        if fmt != "faiss" or not index.is_trained:
+            raise RuntimeError("IndexPreTransform is written in the Faiss layout once trained")
+        chain = [(t.A, t.b, t.d_in, t.d_out, t.is_trained) for t in index.chain]
+        buf = faiss_io.serialize_pretransform(index.d, index.metric_type, chain, _ivfpq_bytes(index.index),
+                                              index.ntotal)
+    elif fmt == "native" or not index.is_trained:
+        _lib.check(_lib.load().ivfpq_save(index._h, str(path).encode()))
+        return
+    elif fmt != "faiss":
+        raise RuntimeError(f"unknown index file format {fmt!r}")
+    else:
+        buf = _ivfpq_bytes(index)
     with open(path, "wb") as f:
         f.write(buf)
 
 
+def _ivfpq_from_dict(z, device):
+    idx = IndexIVFPQ(None, z["d"], z["nlist"], z["M"], z["nbits"], z["metric"], device)
+    if z["is_trained"]:
+        idx.set_trained(z["centroids"], z["codebook"])
+        nonempty = [(l, ids, codes) for l, (ids, codes) in enumerate(z["lists"]) if len(ids)]
+        if nonempty:
+            idx.add_preencoded(np.concatenate([np.full(len(ids), l, np.int64) for l, ids, _ in nonempty]),
+                               np.concatenate([codes for _, _, codes in nonempty]),
+                               np.concatenate([ids for _, ids, _ in nonempty]))
+    idx.nprobe = max(1, min(int(z["nprobe"]), z["nlist"]))
+    return idx
+
+
 def read_index(path, device=None):
-    """Load a Faiss IndexIVFPQ file ("IwPQ") or a CHIVFPQ1 image onto ``device``."""
+    """Load a Faiss IndexIVFPQ ("IwPQ") / IndexPreTransform ("IxPT") file or a
+    CHIVFPQ1 image onto ``device``."""
     device = _default_device() if device is None else device
     if faiss_io.is_faiss_file(path):
         with open(path, "rb") as f:
-            z = faiss_io.parse_ivfpq(f.read())
-        idx = IndexIVFPQ(None, z["d"], z["nlist"], z["M"], z["nbits"], z["metric"], device)
-        if z["is_trained"]:
-            idx.set_trained(z["centroids"], z["codebook"])
-            nonempty = [(l, ids, codes) for l, (ids, codes) in enumerate(z["lists"]) if len(ids)]
-            if nonempty:
-                idx.add_preencoded(np.concatenate([np.full(len(ids), l, np.int64) for l, ids, _ in nonempty]),
-                                   np.concatenate([codes for _, _, codes in nonempty]),
-                                   np.concatenate([ids for _, ids, _ in nonempty]))
-        idx.nprobe = max(1, min(int(z["nprobe"]), z["nlist"]))
-        return idx
+            z = faiss_io.parse_index(f.read())
+        if z["kind"] != "pretransform":
+            return _ivfpq_from_dict(z, device)
+        from .transform import IndexPreTransform, _linear_from_dict
+
+        return IndexPreTransform([_linear_from_dict(t) for t in z["chain"]], _ivfpq_from_dict(z["index"], device))
     h = _lib.c_handle()
     L = _lib.load()
     _lib.check(L.ivfpq_load(str(path).encode(), device, ctypes.byref(h)))

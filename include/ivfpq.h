@@ -98,6 +98,15 @@ int ivfpq_coarse_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, 
 int ivfpq_merge_topk_device(int S, int64_t n, int k, int metric, const float* Din, const int64_t* Iin, float* Dout,
                             int64_t* Iout, void* stream);
 
+/* Linear pre-transform on device buffers (Faiss VectorTransform::apply for OPQMatrix /
+ * LinearTransform: the "OPQ16" of "OPQ16,IVF262144,PQ16", bench_gpu_1bn.py:485-489,
+ * extract_FPGA_required_data.py:162-165): y[i][j] = sum_t x[i][t] * A[j][t] (+ b[j]),
+ * the sum a t-ordered fused-multiply-add chain from 0, bias added last (Faiss uses
+ * sgemm, whose order BLAS leaves open; this is the order of oracle/ivfpq_oracle.c).
+ * AT = A transposed, [d_in][d_out]; b nullable; x [n][d_in], y [n][d_out]. */
+int ivfpq_linear_transform_device(int64_t n, int d_in, int d_out, const float* AT, const float* b, const float* x,
+                                  float* y, void* stream);
+
 /* Per-stage device timing (the nsys stage split of MICRO_GPU_profiling/classify_stages.py:113-181,
  * measured live with HIP events recorded on the launch stream around each stage).
  * get_timing waits for the recorded events, returns per-stage sums in ms and launch counts

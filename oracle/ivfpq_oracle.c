@@ -212,6 +212,22 @@ void or_coarse_search(const float *x, int64_t n, int d, const float *cent, const
     or_coarse_search_metric(x, n, d, cent, cnorm, nlist, nprobe, lists, dis, nthreads, 1);
 }
 
+/* ---------------- linear pre-transform ---------------- */
+
+/* y[i][j] = sum_t x[i][t] A[j][t] (+ b[j]): VectorTransform::apply of an
+ * OPQMatrix / LinearTransform (Faiss LinearTransform::apply_noalloc does this
+ * with sgemm, whose summation order BLAS leaves open; this restatement fixes it
+ * as a t-ordered fmaf chain from 0 with the bias added last -- the order the GPU
+ * kernel uses; parity with Faiss itself is unpinned).  A: [d_out][d_in]. */
+void or_linear_transform(const float *x, int64_t n, int d_in, const float *A, const float *b, int d_out, float *y) {
+    for (int64_t i = 0; i < n; i++)
+        for (int j = 0; j < d_out; j++) {
+            float acc = 0.0f;
+            for (int t = 0; t < d_in; t++) acc = fmaf(x[i * d_in + t], A[(int64_t)j * d_in + t], acc);
+            y[i * d_out + j] = b ? acc + b[j] : acc;
+        }
+}
+
 /* ---------------- PQ tables ---------------- */
 
 /* T3[q][m][j] = <q_m, C_mj>  (ProductQuantizer::compute_inner_prod_table) */

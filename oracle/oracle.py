@@ -47,6 +47,7 @@ def lib():
                                        ctypes.c_int, _i64p, _f32p, ctypes.c_int]
         L.or_coarse_search_metric.argtypes = L.or_coarse_search.argtypes + [ctypes.c_int]
         L.or_ip_table.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
+        L.or_linear_transform.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, _f32p, ctypes.c_int, _f32p]
         L.or_precompute_T1.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int, _f32p]
         L.or_encode.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int, _f32p, _f32p, ctypes.c_int, _f32p,
                                 ctypes.c_int, ctypes.c_int, _i64p, _u8p, ctypes.c_int]
@@ -94,6 +95,19 @@ def norms(x):
     out = np.empty(x.shape[0], np.float32)
     lib().or_norms(_p(x, _f32p), x.shape[0], x.shape[1], _p(out, _f32p))
     return out
+
+
+def linear_transform(x, A, b=None):
+    """y = x A^T (+ b) in the t-ordered fmaf order (or_linear_transform): OPQ apply."""
+    x = _f32(x)
+    A = _f32(A)
+    d_out, d_in = A.shape
+    assert x.shape[1] == d_in
+    y = np.empty((x.shape[0], d_out), np.float32)
+    bb = None if b is None else _f32(b)
+    lib().or_linear_transform(_p(x, _f32p), x.shape[0], d_in, _p(A, _f32p), None if bb is None else _p(bb, _f32p),
+                              d_out, _p(y, _f32p))
+    return y
 
 
 def ip_table(x, codebook):

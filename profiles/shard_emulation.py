@@ -42,6 +42,7 @@ def main():
     full = faiss.index_factory(128, "IVF1024,PQ16")
     full.train(xt)
     full.add(xb)
+    full.nprobe = npb
     sizes = full.invlists.list_sizes()
     xd = torch.from_numpy(xq).cuda()
     ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731

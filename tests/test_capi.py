@@ -59,8 +59,9 @@ def test_invalid_arguments_rejected_before_device():
 def test_factory_and_parameter_parsing():
     assert faiss.index.parse_factory("IVF1024,PQ16") == (1024, 16, 8)
     assert faiss.index.parse_factory("IVF65536,PQ48x8") == (65536, 48, 8)
+    assert faiss.index.parse_factory("OPQ16,IVF1024,PQ16") == (1024, 16, 8, 16, -1)
     with pytest.raises(RuntimeError):
-        faiss.index.parse_factory("OPQ16,IVF1024,PQ16")
+        faiss.index.parse_factory("IVF1024,Flat")
 
     class Fake:
         nprobe = 1
