@@ -155,6 +155,7 @@ struct ivfpq_index {
   hipStream_t stream = nullptr;
   // scratch
   DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
+  DevBuf h_D, h_I, h_Iq, h_Dq;  // device staging of the host-buffer entry points
   // list-major plan workspaces (ivfpq_kernels.h ListPlan)
   DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_tau, p_qmask;
   // Stream ordering of the per-handle workspaces: every device search records
@@ -511,7 +512,8 @@ struct ivfpq_index {
     mark_done(s);
   }
 
-  // host-buffer search (copies in/out on the handle's stream)
+  // host-buffer search (copies in/out on the handle's stream; device staging
+  // buffers persist across calls)
   void search_host(int64_t n, const float* x, int k, float* D, int64_t* I, const int64_t* Iq, const float* Dq,
                    bool preassigned) {
     check_search(n, k);
@@ -519,23 +521,94 @@ struct ivfpq_index {
     order_after_last(stream);
     const int np = nprobe;
     w_x.ensure(sizeof(float) * n * d);
-    DevBuf dD, dI, dIq, dDq;
-    dD.ensure(sizeof(float) * n * k);
-    dI.ensure(sizeof(int64_t) * n * k);
+    h_D.ensure(sizeof(float) * n * k);
+    h_I.ensure(sizeof(int64_t) * n * k);
     HIPCHECK(hipMemcpyAsync(w_x.p, x, sizeof(float) * n * d, hipMemcpyHostToDevice, stream));
     if (preassigned) {
-      dIq.ensure(sizeof(int64_t) * n * np);
-      HIPCHECK(hipMemcpyAsync(dIq.p, Iq, sizeof(int64_t) * n * np, hipMemcpyHostToDevice, stream));
+      h_Iq.ensure(sizeof(int64_t) * n * np);
+      HIPCHECK(hipMemcpyAsync(h_Iq.p, Iq, sizeof(int64_t) * n * np, hipMemcpyHostToDevice, stream));
       if (Dq) {
-        dDq.ensure(sizeof(float) * n * np);
-        HIPCHECK(hipMemcpyAsync(dDq.p, Dq, sizeof(float) * n * np, hipMemcpyHostToDevice, stream));
+        h_Dq.ensure(sizeof(float) * n * np);
+        HIPCHECK(hipMemcpyAsync(h_Dq.p, Dq, sizeof(float) * n * np, hipMemcpyHostToDevice, stream));
       }
     }
-    search_dev(n, w_x.as<float>(), k, dD.as<float>(), dI.as<int64_t>(), dIq.as<int64_t>(),
-               Dq ? dDq.as<float>() : nullptr, preassigned, stream);
-    HIPCHECK(hipMemcpyAsync(D, dD.p, sizeof(float) * n * k, hipMemcpyDeviceToHost, stream));
-    HIPCHECK(hipMemcpyAsync(I, dI.p, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, stream));
+    search_dev(n, w_x.as<float>(), k, h_D.as<float>(), h_I.as<int64_t>(), h_Iq.as<int64_t>(),
+               Dq ? h_Dq.as<float>() : nullptr, preassigned, stream);
+    HIPCHECK(hipMemcpyAsync(D, h_D.p, sizeof(float) * n * k, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(I, h_I.p, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, stream));
     HIPCHECK(hipStreamSynchronize(stream));
+  }
+
+  // One FaissServer request in the ralm wire format
+  // (ralm/retriever/serialization_utils.py): header integers big-endian
+  // (BYTE_ORDER_PY = 'big', :5), arrays in native order (tobytes, :59, :86-87).
+  //   with_lists 0: k | queries f32[B][dim]                      (encode_request :38-67)
+  //   with_lists 1: B, dim, nprobe, k | queries | lists i64[B][np] (encode_request_with_lists :69-94)
+  // The answer is I i64[B][k] | D f32[B][k] (encode_answer :223-258), copied from
+  // HBM straight into the answer buffer.  Shape checks follow decode_request*
+  // (asserts at :211-213) and FaissServer.start (faiss_server.py:241-277).
+  void serve(const uint8_t* msg, int64_t len, int with_lists, int B, int dim, int np, uint8_t* ans, int64_t cap,
+             int64_t* ans_len) {
+    auto be32 = [](const uint8_t* p) {
+      return (int64_t)(int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]);
+    };
+    require(B > 0 && dim == d, "server shape: batch_size must be > 0 and dim must equal the index's d");
+    const int64_t qbytes = (int64_t)B * dim * 4;
+    int64_t k;
+    const uint8_t* qp;
+    const uint8_t* lp = nullptr;
+    if (with_lists) {
+      require(np >= 1, "nprobe must be >= 1");
+      require(len == 16 + qbytes + (int64_t)B * np * 8,
+              "request length " + std::to_string(len) + " != request_message_length_with_lists(" +
+                  std::to_string(B) + ", " + std::to_string(dim) + ", " + std::to_string(np) + ")");
+      require(be32(msg) == B && be32(msg + 4) == dim && be32(msg + 8) == np,
+              "request header (batch_size, dim, nprobe) does not match the server's shape");
+      k = be32(msg + 12);
+      qp = msg + 16;
+      lp = msg + 16 + qbytes;
+    } else {
+      require(len == 4 + qbytes, "request length " + std::to_string(len) + " != request_message_length(" +
+                                     std::to_string(B) + ", " + std::to_string(dim) + ")");
+      k = be32(msg);
+      qp = msg + 4;
+    }
+    require(k >= 1 && k <= kMaxK, "k in the request must be in [1, " + std::to_string(kMaxK) + "]");
+    const int64_t need = (int64_t)B * k * 12;
+    require(ans != nullptr && cap >= need, "answer buffer holds " + std::to_string(cap) + " bytes, the answer needs " +
+                                               std::to_string(need));
+    check_search(B, (int)k);
+    order_after_last(stream);
+    w_x.ensure(qbytes);
+    h_D.ensure(sizeof(float) * B * k);
+    h_I.ensure(sizeof(int64_t) * B * k);
+    HIPCHECK(hipMemcpyAsync(w_x.p, qp, qbytes, hipMemcpyHostToDevice, stream));
+    if (with_lists) {
+      // the list ids sit at an arbitrary byte offset of the message: validate on the host, copy as bytes
+      for (int64_t i = 0; i < (int64_t)B * np; i++) {
+        int64_t l;
+        std::memcpy(&l, lp + 8 * i, 8);
+        require(l < nlist, "list id out of range in the request");
+      }
+      const int saved = nprobe;
+      nprobe = np;  // search_preassigned scans list_nos.shape[1] probes
+      h_Iq.ensure(sizeof(int64_t) * B * np);
+      HIPCHECK(hipMemcpyAsync(h_Iq.p, lp, sizeof(int64_t) * B * np, hipMemcpyHostToDevice, stream));
+      try {
+        search_dev(B, w_x.as<float>(), (int)k, h_D.as<float>(), h_I.as<int64_t>(), h_Iq.as<int64_t>(), nullptr, true,
+                   stream);
+      } catch (...) {
+        nprobe = saved;
+        throw;
+      }
+      nprobe = saved;
+    } else {
+      search_dev(B, w_x.as<float>(), (int)k, h_D.as<float>(), h_I.as<int64_t>(), nullptr, nullptr, false, stream);
+    }
+    HIPCHECK(hipMemcpyAsync(ans, h_I.p, sizeof(int64_t) * B * k, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipMemcpyAsync(ans + (int64_t)B * k * 8, h_D.p, sizeof(float) * B * k, hipMemcpyDeviceToHost, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+    if (ans_len) *ans_len = need;
   }
 };
 
@@ -793,6 +866,17 @@ int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, i
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     h->search_dev(n, x, k, D, I, Iq, Dq, true, (hipStream_t)stream);
+  });
+}
+
+int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int with_lists, int batch_size, int dim,
+                        int nprobe, uint8_t* answer, int64_t answer_cap, int64_t* answer_len) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(msg != nullptr, "null request message");
+    h->serve(msg, msg_len, with_lists, batch_size, dim, nprobe, answer, answer_cap, answer_len);
   });
 }
 

@@ -45,6 +45,8 @@ SIGNATURES = {
     "ivfpq_search_preassigned_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "ivfpq_serve_request": (ctypes.c_int, [c_handle, c_u8p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, c_u8p, ctypes.c_int64, c_i64p]),
     "ivfpq_coarse_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
     "ivfpq_merge_topk_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,

@@ -387,6 +387,28 @@ class IndexIVFPQ:
                                                         _ptr(I, _lib.c_i64p)))
         return D, I
 
+    def serve_request(self, msg, batch_size, dim, with_lists=False, nprobe=None, out=None):
+        """One FaissServer request (RALM wire format, ``faiss_amd.wire``) in, the
+        encoded answer out: decode + search (or search_preassigned) + encode in
+        one native call (``ivfpq_serve_request``).  ``out``: optional writable
+        buffer of at least ``answer_message_len(k, batch_size)`` bytes, filled
+        in place; returns the answer as ``bytearray`` (or ``out``'s view)."""
+        buf = np.frombuffer(msg, np.uint8)
+        np_ = int(self.nprobe if nprobe is None else nprobe)
+        if out is None:
+            from .wire import peek_k
+
+            k = peek_k(msg, with_lists)
+            out = bytearray(max(1, batch_size * k * 12))
+        ans = np.frombuffer(out, np.uint8)
+        if not ans.flags.writeable:
+            raise RuntimeError("answer buffer must be writable")
+        ln = ctypes.c_int64(0)
+        _lib.check(_lib.load().ivfpq_serve_request(self._h, _ptr(buf, _lib.c_u8p), buf.size, int(bool(with_lists)),
+                                                   int(batch_size), int(dim), np_, _ptr(ans, _lib.c_u8p), ans.size,
+                                                   ctypes.byref(ln)))
+        return out if len(out) == ln.value else memoryview(out)[:ln.value]
+
     # ------------------------------------------------------------ stage timing
     STAGES = ("coarse", "tables", "scan", "lists")
 

@@ -87,6 +87,20 @@ int ivfpq_search_preassigned(ivfpq_index* h, int64_t n, const float* x, int k, c
 int ivfpq_search_device(ivfpq_index* h, int64_t n, const float* x, int k, float* D, int64_t* I, void* stream);
 int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq,
                                     const float* Dq, float* D, int64_t* I, void* stream);
+/* FaissServer request handling in the RALM wire format: decode_request[_with_lists] +
+ * retrieve / retrieve_with_lists + encode_answer (ralm/server/faiss_server.py:170-277;
+ * formats ralm/retriever/serialization_utils.py:17-35, 38-94, 173-258).  Header integers
+ * are big-endian int32, arrays native-order:
+ *   with_lists = 0: msg = k | queries f32 [batch_size][dim]               -> search (nprobe of the index)
+ *   with_lists = 1: msg = batch_size, dim, nprobe, k | queries | lists i64 [batch_size][nprobe]
+ *                                                                          -> search_preassigned, Dq = NULL
+ * The answer is written to `answer`: I i64 [batch_size][k] then D f32 [batch_size][k];
+ * *answer_len (nullable) = batch_size * k * 12.  msg_len must equal the format's message
+ * length for (batch_size, dim[, nprobe]), and the with-lists header must match them
+ * (decode_request_with_lists asserts, serialization_utils.py:211-213). */
+int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int with_lists, int batch_size, int dim,
+                        int nprobe, uint8_t* answer, int64_t answer_cap, int64_t* answer_len);
+
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing
  * Iq [n][nprobe] / Dq [n][nprobe]; and the per-query inner-product table T3. */
