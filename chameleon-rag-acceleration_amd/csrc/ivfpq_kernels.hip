@@ -1950,6 +1950,128 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       return;
     }
   }
+  if constexpr (R >= 2) {
+    // k > 64, nprobe <= 64: bound first, then merge only the entries under the bound.
+    // S = the first s entries of each of the L = 4 nprobe sorted partial lists
+    // (L s >= k); S is a subset of all entries, so its k-th smallest key T bounds
+    // the final k-th key.  T is found by a bisection on the order-preserving
+    // integer of the keys (32 ballot-count rounds).  Then every list's prefix
+    // <= T is compacted into LDS and only those candidates get their labels
+    // looked up and enter the (key, label) top-k.  Too many candidates (ties)
+    // fall through to the full merge below.
+    constexpr int CAP = 128 * R;  // candidates per wave (>= 2k)
+    constexpr int SV = R + 4;     // S slots per lane: L s <= k + L - 1 <= 64 R + 255
+    __shared__ float cd_s[4][CAP];
+    __shared__ int64_t cp_s[4][CAP];
+    if (np <= 64) {
+      const int wave = threadIdx.x >> 6;
+      const int L = 4 * np;
+      const int s = (k + L - 1) / L;
+      const int NS = L * s;
+      const uint64_t qm = pl.qmask[q];
+      auto ukey = [](float v) __attribute__((always_inline)) {
+        return (uint32_t)f2ord(v + 0.0f) ^ 0x80000000u;  // unsigned order == float order (-0 folded)
+      };
+      uint32_t u[SV];
+      int nvalid = 0;
+#pragma unroll
+      for (int t = 0; t < SV; t++) {
+        const int e = t * 64 + lane;
+        const int j = e % L, i = e / L;
+        const bool in = e < NS && ((qm >> (j >> 2)) & 1);
+        const int64_t at = ((q * np + (j >> 2)) * 4 + (j & 3)) * (int64_t)k + (in ? i : 0);
+        const int64_t pos = in ? pl.partI[at] : -1;
+        const float dv = in ? pl.partD[at] : kInf;
+        const bool ok = pos >= 0;
+        u[t] = ok ? ukey(dv) : 0xFFFFFFFFu;
+        nvalid += __popcll(__builtin_amdgcn_ballot_w64(ok));
+      }
+      uint32_t Tu = 0xFFFFFFFEu;  // fewer than k entries in S: every valid entry is a candidate
+      if (nvalid >= k) {
+        uint32_t lo = 0, hi = 0xFFFFFFFEu;
+        while (lo < hi) {
+          const uint32_t mid = lo + ((hi - lo) >> 1);
+          int cnt = 0;
+#pragma unroll
+          for (int t = 0; t < SV; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u[t] <= mid));
+          if (cnt >= k) hi = mid; else lo = mid + 1;
+        }
+        Tu = lo;
+      }
+      // per list: the length of its prefix <= T (lists sorted, valid entries first)
+      int c[4] = {0, 0, 0, 0};
+      int mine = 0;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int j = t * 64 + lane;
+        if (j < L && ((qm >> (j >> 2)) & 1)) {
+          const int64_t base = ((q * np + (j >> 2)) * 4 + (j & 3)) * (int64_t)k;
+          int n = 0;
+          bool go = true;
+          while (go && n < k) {
+            float dv[8];
+            int64_t pv[8];
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+              const int i = min(n + h, k - 1);
+              dv[h] = pl.partD[base + i];
+              pv[h] = pl.partI[base + i];
+            }
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+              if (go && n < k && pv[h] >= 0 && ukey(dv[h]) <= Tu) n++;
+              else go = false;
+            }
+          }
+          c[t] = n;
+          mine += n;
+        }
+      }
+      const int incl = wave_incl_scan(mine, lane);
+      const int C = __builtin_amdgcn_readlane(incl, 63);
+      if (C <= CAP) {
+        int o = incl - mine;
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int j = t * 64 + lane;
+          if (c[t] > 0) {
+            const int64_t base = ((q * np + (j >> 2)) * 4 + (j & 3)) * (int64_t)k;
+            for (int i = 0; i < c[t]; i++, o++) {
+              cd_s[wave][o] = pl.partD[base + i];
+              cp_s[wave][o] = pl.partI[base + i];
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        WaveTopK<R> tb;
+        tb.init(k);
+        for (int b0 = 0; b0 < C; b0 += 64) {
+          const int e = b0 + lane;
+          const float dv = e < C ? cd_s[wave][e] : kInf;
+          const int64_t id = e < C ? a.ids[cp_s[wave][e]] : kSentinelId;
+          const bool pass = e < C && lexless(dv, id, tb.td, tb.ti);
+          const uint64_t mask = __ballot(pass);
+          if (!mask) continue;
+          if (__popcll(mask) > 6)
+            bulk_merge_rows(tb, pass ? dv : kInf, pass ? id : kSentinelId, lane);
+          else
+            tb.insert(mask, dv, id, lane);
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int idx = r * 64 + lane;
+          if (idx < k) {
+            const bool empty = tb.id[r] == kSentinelId;
+            a.outD[q * k + idx] = empty ? pad : sgn * tb.d[r];
+            a.outI[q * k + idx] = empty ? -1 : tb.id[r];
+          }
+        }
+        return;
+      }
+    }
+  }
   WaveTopK<R> tk;
   tk.init(k);
   const int per_probe = 4 * k;
