@@ -150,7 +150,8 @@ struct ivfpq_index {
   int64_t ntotal = 0;
   int64_t next_id = 0;
 
-  DevBuf d_cent, d_centT, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off;
+  DevBuf d_cent, d_centT, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off, d_order;
+  std::vector<int32_t> order_host;
   bool dirty = true;
   hipStream_t stream = nullptr;
   // scratch
@@ -206,6 +207,7 @@ struct ivfpq_index {
     pl.partI = p_I.as<int64_t>();
     pl.tauq = p_tau.as<int32_t>();
     pl.qmask = p_qmask.as<uint64_t>();
+    pl.order = d_order.p ? d_order.as<int32_t>() : nullptr;
     return pl;
   }
 
@@ -376,6 +378,21 @@ struct ivfpq_index {
         std::memcpy(codes.data() + (off[l] + i) * M, lcodes[l].data() + perm[i] * M, M);
         ids[off[l] + i] = lid[perm[i]];
       }
+    }
+    // Scheduling order of the shard's lists: largest first (the list scan takes
+    // items in this order within each kind, so the items that finish last are the
+    // short ones: longest-processing-time-first bounds the persistent grid's tail).
+    {
+      const int nloc = std::max(list_hi - list_lo, 1);
+      std::vector<int32_t> order(nloc);
+      for (int j = 0; j < nloc; j++) order[j] = j;
+      if (list_hi > list_lo)
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+          return lids[list_lo + a].size() > lids[list_lo + b].size();
+        });
+      d_order.ensure(sizeof(int32_t) * nloc);
+      HIPCHECK(hipMemcpyAsync(d_order.p, order.data(), sizeof(int32_t) * nloc, hipMemcpyHostToDevice, stream));
+      order_host = std::move(order);  // kept alive until the copy completes (synchronized below)
     }
     d_codes.ensure(std::max<size_t>(16, codes.size()));
     d_ids.ensure(std::max<size_t>(16, sizeof(int64_t) * ids.size()));
@@ -824,6 +841,7 @@ int ivfpq_set_list_range(ivfpq_index* h, int lo, int hi) {
     require(h->ntotal == 0, "set the list range before adding vectors");
     h->list_lo = lo;
     h->list_hi = hi;
+    h->dirty = true;  // the device image (list order) follows the range
   });
 }
 

@@ -82,6 +82,7 @@ struct ListPlan {
   int32_t* tauq;     // [nq] running k-th key per query (order-preserving int of the float, atomicMin)
   uint64_t* qmask;   // [nq] probes the scan covers (nprobe <= 64): bit p = pair (q, p) is scanned
   int grid;          // persistent list-scan workgroups (multiple of 8)
+  const int32_t* order = nullptr;  // [nloc] item order of the lists within a kind (nullable = list order)
 };
 
 struct ScanArgs {

@@ -1194,10 +1194,16 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
   const int tid = threadIdx.x;
   // per-list exclusive prefix of the item counts, both kinds, in chunks of 1024 lists
   int ca = 0, cb = 0;
+#ifdef PLAN_LIST_ORDER  // items of a kind in list order (A/B)
+  const int32_t* ord = nullptr;
+#else  // items of a kind by list size, largest first
+  const int32_t* ord = pl.order;
+#endif
   for (int j0 = 0; j0 < nloc; j0 += PLAN_T) {
-    const int j = j0 + tid;
-    const int a = j < nloc ? (min(pl.cnt[j], pl.cap) + G - 1) / G : 0;
-    const int b = j < nloc ? (min(pl.cnt[nloc + j], pl.cap) + G - 1) / G : 0;
+    const int j = j0 + tid;  // rank in the scheduling order
+    const int jl = j < nloc ? (ord ? ord[j] : j) : 0;
+    const int a = j < nloc ? (min(pl.cnt[jl], pl.cap) + G - 1) / G : 0;
+    const int b = j < nloc ? (min(pl.cnt[nloc + jl], pl.cap) + G - 1) / G : 0;
     int ea, eb, ta, tb;
     block_scan2(a, b, ea, eb, ta, tb, ws);
     if (j < nloc) {
@@ -1227,7 +1233,7 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
     else
       hi_i = mid;
   }
-  write_item(pl, list_off, lo, nloc, G, e, lo_i, kind, ek - exk[lo_i]);
+  write_item(pl, list_off, lo, nloc, G, e, ord ? ord[lo_i] : lo_i, kind, ek - exk[lo_i]);
 }
 
 __global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
