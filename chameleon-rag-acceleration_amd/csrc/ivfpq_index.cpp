@@ -186,7 +186,7 @@ struct ivfpq_index {
     ListPlan pl;
     pl.cap = (int)nq;
     pl.max_items = list_scan_max_items(nq * np, nloc, G);
-    pl.grid = scan_lists_grid();
+    pl.grid = scan_lists_grid(M, k);
     if (!p_cnt.p || p_cnt.bytes < sizeof(int32_t) * 2 * nloc) {
       // kept zero between batches by k_scan_lists; zeroed once here
       p_cnt.ensure(sizeof(int32_t) * 2 * nloc);

@@ -117,7 +117,7 @@ void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int 
 
 int list_scan_group(int M, int k);  // pairs per work item (G) used for (M, k)
 int list_scan_max_items(int64_t npairs, int nloc, int G);
-int scan_lists_grid();  // persistent grid size for the device (2 workgroups per CU)
+int scan_lists_grid(int M, int k);  // persistent grid size for the device (2-3 workgroups per CU by LDS)
 bool scan_supported_M(int M);
 // list scan + probe merge; ev_lists (nullable): two events recorded around the list-scan kernel alone
 void launch_scan_lists(const ScanArgs& a, const ListPlan& plan, hipStream_t s, hipEvent_t* ev_lists = nullptr);

@@ -1773,7 +1773,20 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       }
       int t = 0;
       bool pend = false;  // a drain requested by the last chunk
-      while (true) {
+      // Most super-batches of a query that already has a bound admit nothing:
+      // one compare per (chunk, pair) and a single ballot decide that, and the
+      // per-chunk admission below runs only when some lane passes.
+      bool anyc = false;
+#pragma unroll
+      for (int j = 0; j < JB; j++) {
+        if (j < tn) {  // wave-uniform
+          const bool valid = sb + j * 256 + wave * 64 + lane < n;
+#pragma unroll
+          for (int g = 0; g < G; g++) anyc = anyc || (valid && dis[j][g] <= bound[g]);
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(anyc) == 0) t = tn;  // nothing to admit in this super-batch
+      while (t < tn) {
         int stop = tn;       // first chunk not yet admitted
         bool want = false;   // drain requested
         bool go = true;
@@ -1960,19 +1973,22 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     // k > 64, nprobe <= 64: bound first, then merge only the entries under the bound.
     // S = the first s entries of each of the L = 4 nprobe sorted partial lists
     // (L s >= k); S is a subset of all entries, so its k-th smallest key T bounds
-    // the final k-th key.  T is found by a bisection on the order-preserving
-    // integer of the keys (32 ballot-count rounds).  Then every list's prefix
-    // <= T is compacted into LDS and only those candidates get their labels
-    // looked up and enter the (key, label) top-k.  Too many candidates (ties)
-    // fall through to the full merge below.
-    constexpr int CAP = 128 * R;  // candidates per wave (>= 2k)
-    constexpr int SV = R + 4;     // S slots per lane: L s <= k + L - 1 <= 64 R + 255
+    // the final k-th key -- and equals it whenever no list contributes more than
+    // s entries to the top-k, so s is as large as SV slots per lane allow.  T is
+    // found by a bisection on the order-preserving integer of the keys (32
+    // ballot-count rounds).  Then every list's prefix <= T is compacted into LDS
+    // and only those candidates get their labels looked up and enter the
+    // (key, label) top-k.  Too many candidates (ties) fall through to the full
+    // merge below.
+    constexpr int CAP = R <= 8 ? 1024 : 128 * R;  // candidates per wave (>= 2k)
+    constexpr int CAP2 = R <= 8 ? CAP : 0;         // second bisection over up to CAP2 candidates
+    constexpr int SV = R + 4 > 16 ? R + 4 : 16;  // S slots per lane (64 SV >= k + 256 > k + L - 1)
     __shared__ float cd_s[4][CAP];
     __shared__ int64_t cp_s[4][CAP];
     if (np <= 64) {
       const int wave = threadIdx.x >> 6;
       const int L = 4 * np;
-      const int s = (k + L - 1) / L;
+      const int s = min(k, 64 * SV / L);  // L s >= 64 SV - L + 1 > k
       const int NS = L * s;
       const uint64_t qm = pl.qmask[q];
       auto ukey = [](float v) __attribute__((always_inline)) {
@@ -2034,7 +2050,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
         }
       }
       const int incl = wave_incl_scan(mine, lane);
-      const int C = __builtin_amdgcn_readlane(incl, 63);
+      int C = __builtin_amdgcn_readlane(incl, 63);
       if (C <= CAP) {
         int o = incl - mine;
 #pragma unroll
@@ -2051,19 +2067,74 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if constexpr (CAP2 > 0) {
+          // A list holding more than s of the top-k leaves T loose: tighten it by a
+          // second bisection over the compacted candidates (held in registers),
+          // then keep only those <= T2 at the front of the buffer (in place: an
+          // entry only moves to a lower index, and every slot is read by the whole
+          // wave before it is written).
+          if (C > 2 * k) {
+            uint32_t u2[CAP2 / 64];
+#pragma unroll
+            for (int t = 0; t < CAP2 / 64; t++) {
+              const int e = t * 64 + lane;
+              u2[t] = e < C ? ukey(cd_s[wave][e]) : 0xFFFFFFFFu;
+            }
+            uint32_t lo = 0, hi = 0xFFFFFFFEu;
+            while (lo < hi) {
+              const uint32_t mid = lo + ((hi - lo) >> 1);
+              int cnt = 0;
+#pragma unroll
+              for (int t = 0; t < CAP2 / 64; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u2[t] <= mid));
+              if (cnt >= k) hi = mid; else lo = mid + 1;
+            }
+            int n2 = 0;
+#pragma unroll
+            for (int t = 0; t < CAP2 / 64; t++) {
+              const int e = t * 64 + lane;
+              const bool keep = e < C && u2[t] <= lo;
+              const uint64_t mk = __builtin_amdgcn_ballot_w64(keep);
+              if (mk) {
+                const float dv = cd_s[wave][e < C ? e : 0];
+                const int64_t pv = cp_s[wave][e < C ? e : 0];
+                __builtin_amdgcn_wave_barrier();
+                if (keep) {
+                  const int at = n2 + __popcll(mk & ((1ull << lane) - 1));
+                  cd_s[wave][at] = dv;
+                  cp_s[wave][at] = pv;
+                }
+                n2 += __popcll(mk);
+              }
+            }
+            C = n2;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
+        }
         WaveTopK<R> tb;
         tb.init(k);
-        for (int b0 = 0; b0 < C; b0 += 64) {
-          const int e = b0 + lane;
-          const float dv = e < C ? cd_s[wave][e] : kInf;
-          const int64_t id = e < C ? a.ids[cp_s[wave][e]] : kSentinelId;
-          const bool pass = e < C && lexless(dv, id, tb.td, tb.ti);
-          const uint64_t mask = __ballot(pass);
-          if (!mask) continue;
-          if (__popcll(mask) > 6)
-            bulk_merge_rows(tb, pass ? dv : kInf, pass ? id : kSentinelId, lane);
-          else
-            tb.insert(mask, dv, id, lane);
+        for (int g0 = 0; g0 < C; g0 += 64 * 4) {
+          // labels of up to 4 batches in flight at once
+          int64_t idb[4];
+          float db[4];
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const int e = g0 + b * 64 + lane;
+            db[b] = e < C ? cd_s[wave][e] : kInf;
+            idb[b] = e < C ? a.ids[cp_s[wave][e]] : kSentinelId;
+          }
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const int e = g0 + b * 64 + lane;
+            const bool pass = e < C && lexless(db[b], idb[b], tb.td, tb.ti);
+            const uint64_t mask = __ballot(pass);
+            if (!mask) continue;
+            if (__popcll(mask) > 6)
+              bulk_merge_rows(tb, pass ? db[b] : kInf, pass ? idb[b] : kSentinelId, lane);
+            else
+              tb.insert(mask, db[b], idb[b], lane);
+          }
         }
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -2307,11 +2378,26 @@ void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int 
 
 bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 || M == 64; }
 
+#ifndef SCAN_G_MAX
+#define SCAN_G_MAX 4  // pairs per work item (A/B builds may lower it)
+#endif
+// Pairs per work item: G LUTs of M x 256 floats interleaved in LDS (<= 64 KB),
+// G x R <= 8 (the per-wave top-k state).  For k > 64 at M <= 16, G = 2 and three
+// workgroups per CU beat G = 4 with two (k = 100 at C2: 174 vs 225 us, r02 A/B).
+constexpr int scan_group(int M, int R) {
+  return (SCAN_G_MAX >= 4 && M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16)) ? 4
+         : (SCAN_G_MAX >= 2 && M * 1024 * 2 <= 65536 && 2 * R <= 8)                      ? 2
+                                                                                          : 1;
+}
 int list_scan_group(int M, int k) {
   const int R = rows_for(k);
-  int G = 4;
-  while (G > 1 && (M * 1024 * G > 65536 || G * R > 8)) G >>= 1;
-  return G;
+  switch (R) {
+    case 1: return scan_group(M, 1);
+    case 2: return scan_group(M, 2);
+    case 4: return scan_group(M, 4);
+    case 8: return scan_group(M, 8);
+    default: return scan_group(M, 16);
+  }
 }
 
 int list_scan_max_items(int64_t npairs, int nloc, int G) {
@@ -2320,23 +2406,30 @@ int list_scan_max_items(int64_t npairs, int nloc, int G) {
   return (int)v;
 }
 
-int scan_lists_grid() {
-  static int grid = 0;
-  if (!grid) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-#ifndef SCAN_WG_PER_CU
-#define SCAN_WG_PER_CU 2
-#endif
-    grid = std::max(8, (SCAN_WG_PER_CU * cus + 7) / 8 * 8);
+int scan_lists_grid(int M, int k) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    cus = n;
   }
-  return grid;
+#ifdef SCAN_WG_PER_CU
+  const int per_cu = SCAN_WG_PER_CU;
+#else
+  // workgroups per CU the LDS allows (LUTs + candidate queues), at most 3
+  const int lds = M * 256 * 4 * list_scan_group(M, k) + 4 * QCAP * 8 + 64;
+  const int per_cu = std::max(1, std::min(3, 160 * 1024 / lds));
+#endif
+  return std::max(8, (per_cu * cus + 7) / 8 * 8);
 }
 
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
-  constexpr int G = (M * 1024 * 4 <= 65536 && 4 * R <= 8) ? 4 : (M * 1024 * 2 <= 65536 && 2 * R <= 8) ? 2 : 1;
-  constexpr int JB = M <= 16 ? 8 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs), even
+  constexpr int G = scan_group(M, R);
+#ifndef SCAN_JB16
+#define SCAN_JB16 8  // A/B builds may lower it
+#endif
+  constexpr int JB = M <= 16 ? SCAN_JB16 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs), even
   if (ev) (void)hipEventRecord(ev[0], s);
   hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
 #ifdef SCAN_TWICE  // diagnostic build only: re-scan with every query's tau already tight
