@@ -1187,6 +1187,44 @@ __device__ __forceinline__ void write_item(const ListPlan& pl, const int64_t* __
   rp[3] = make_int4(r[12], r[13], r[14], r[15]);
 }
 
+// The items of one list when its first-probe pairs (kind 0: c0 of them) and
+// other pairs (c1) share items: slots 0..c-1 run over the kind-0 bucket, then
+// the kind-1 bucket.  The first ceil(c0 / G) items (every first-probe pair, the
+// free slots filled with other pairs of the list) are scheduled in the first
+// phase; the rest after every list's first phase.
+__device__ __forceinline__ void write_item_mixed(const ListPlan& pl, const int64_t* __restrict__ list_off, int lo,
+                                                 int nloc, int G, int rec, int jj, int phase, int t) {
+  const int c0 = min(pl.cnt[jj], pl.cap), c1 = min(pl.cnt[nloc + jj], pl.cap);
+  const int c = c0 + c1;
+  const int cov = min(c, ((c0 + G - 1) / G) * G);  // slots of the first-phase items
+  const int s0 = (phase ? cov : 0) + t * G;
+  const int cnt = min(G, (phase ? c : cov) - s0);
+  const int64_t l = lo + jj;
+  const int64_t beg = list_off[l];
+  int r[16];
+  r[0] = (int)l;
+  r[1] = cnt;
+  r[2] = (int)(list_off[l + 1] - beg);
+  r[3] = (int)(uint32_t)(uint64_t)beg;
+  r[4] = (int)(uint32_t)((uint64_t)beg >> 32);
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    int2 v = make_int2(0, 0);
+    const int sl = s0 + g;
+    if (g < cnt) v = sl < c0 ? pl.bucket[((int64_t)jj * 2) * pl.cap + sl] : pl.bucket[((int64_t)jj * 2 + 1) * pl.cap + sl - c0];
+    r[5 + g] = v.x;
+    r[9 + g] = v.y;
+  }
+  r[13] = phase;
+  r[14] = 0;
+  r[15] = 0;
+  int4* rp = reinterpret_cast<int4*>(pl.recs + (int64_t)rec * 16);
+  rp[0] = make_int4(r[0], r[1], r[2], r[3]);
+  rp[1] = make_int4(r[4], r[5], r[6], r[7]);
+  rp[2] = make_int4(r[8], r[9], r[10], r[11]);
+  rp[3] = make_int4(r[12], r[13], r[14], r[15]);
+}
+
 __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
                                                              int nloc, int G) {
   __shared__ int ex[2][kPlanSmall + 1];
@@ -1202,8 +1240,15 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
   for (int j0 = 0; j0 < nloc; j0 += PLAN_T) {
     const int j = j0 + tid;  // rank in the scheduling order
     const int jl = j < nloc ? (ord ? ord[j] : j) : 0;
+#ifndef PLAN_MIX_KINDS  // kind-0 and kind-1 pairs in separate items
     const int a = j < nloc ? (min(pl.cnt[jl], pl.cap) + G - 1) / G : 0;
     const int b = j < nloc ? (min(pl.cnt[nloc + jl], pl.cap) + G - 1) / G : 0;
+#else  // (A/B, r02: within noise at C2) first-phase items: the kind-0 pairs plus kind-1 pairs in their free slots
+    const int c0 = j < nloc ? min(pl.cnt[jl], pl.cap) : 0;
+    const int cc = j < nloc ? c0 + min(pl.cnt[nloc + jl], pl.cap) : 0;
+    const int a = (c0 + G - 1) / G;
+    const int b = (cc - min(cc, a * G) + G - 1) / G;
+#endif
     int ea, eb, ta, tb;
     block_scan2(a, b, ea, eb, ta, tb, ws);
     if (j < nloc) {
@@ -1233,7 +1278,11 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
     else
       hi_i = mid;
   }
+#ifndef PLAN_MIX_KINDS
   write_item(pl, list_off, lo, nloc, G, e, ord ? ord[lo_i] : lo_i, kind, ek - exk[lo_i]);
+#else
+  write_item_mixed(pl, list_off, lo, nloc, G, e, ord ? ord[lo_i] : lo_i, kind, ek - exk[lo_i]);
+#endif
 }
 
 __global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
