@@ -136,6 +136,7 @@ void kmeans_update(const float* x, int64_t n, int d, int k, const int64_t* assig
 }
 
 constexpr size_t kChunkBytes = size_t(256) << 20;  // bound for [rows][cols] fp32 scratch
+constexpr int kSegmentedNlist = 8192;  // from this nlist on, the coarse quantizer never writes the key matrix
 
 }  // namespace
 
@@ -157,6 +158,7 @@ struct ivfpq_index {
   // scratch
   DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
   DevBuf h_D, h_I, h_Iq, h_Dq;  // device staging of the host-buffer entry points
+  DevBuf w_cand;                // segment candidates of the large-nlist coarse quantizer
   // list-major plan workspaces (ivfpq_kernels.h ListPlan)
   DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_tau, p_qmask;
   // Stream ordering of the per-handle workspaces: every device search records
@@ -435,6 +437,13 @@ struct ivfpq_index {
   // returned; otherwise the caller plans with launch_plan_count.
   bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
                      const ListPlan* plan = nullptr, float* T3out = nullptr) {
+    if (nlist >= kSegmentedNlist && np <= 64) {  // large nlist: no [c][nlist] key matrix
+      w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist) * np);
+      if (T3out) launch_ip_table(x, c, d, d_cb.as<float>(), M, ksub, T3out, s);
+      launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, w_cand.as<uint64_t>(), dis,
+                              lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
+      return plan != nullptr;
+    }
     w_dist.ensure(sizeof(float) * c * nlist);
     launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, w_dist.as<float>(), s, ip(), T3out,
                        d_cb.as<float>(), M);

@@ -707,6 +707,93 @@ struct CoarseT3 {
   int nblk = 0;  // T3 workgroups
 };
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int NTL = GC / 64;  // 16 x 16 MFMA tiles per wave (32 centroids)
+
+// Stage the A operand of a key tile (rows q0..q0+15 transposed, zero-padded to
+// dk) and |x_q|^2 in Faiss tree order into LDS (xs [dk][16], xn [16] + 128
+// floats of scratch).  Ends with the block barrier that publishes xs; xn is
+// published by the caller's next barrier.
+__device__ __forceinline__ void coarse_stage_queries(float* xs, float* xn, const float* __restrict__ x, int64_t q0,
+                                                     int64_t nq, int d, int dk, int tid) {
+  fill_cols(xs, x, q0, nq, d, dk, tid);
+  __syncthreads();
+  // with d % 8 == 0 the 8 lane sums of each query are 8 independent sequential
+  // chains (threads i * 8 + j), folded by 16 threads
+  float* a8 = xn + GQ;  // [GQ][8]
+  if (d % 8 == 0) {
+    if (tid < GQ * 8) {
+      const int i = tid >> 3, j = tid & 7;
+      float acc8 = 0.f;
+      for (int k = j; k < d; k += 8) {
+        const float v = xs[k * GQ + i];
+        acc8 = acc8 + v * v;
+      }
+      a8[i * 8 + j] = acc8;
+    }
+    __syncthreads();
+    if (tid < GQ) {
+      const float* r = a8 + tid * 8;
+      const float h0 = (r[4] + r[0]) + (r[5] + r[1]);
+      const float h1 = (r[6] + r[2]) + (r[7] + r[3]);
+      xn[tid] = h0 + h1;
+    }
+  } else if (tid < GQ) {
+    xn[tid] = tree<K_NORM>([&](int t) { return xs[t * GQ + tid]; }, [&](int t) { return xs[t * GQ + tid]; }, d);
+  }
+}
+
+// acc[t] = the wave's 16 x 16 tiles <x_q, c> for its 16 queries (A rows arow0 ..
+// arow0 + 15 of xs [dk][lda]) and centroids c0 + 16 t .. + 15, accumulated by
+// v_mfma_f32_16x16x4_f32 in ascending k (rounds like the oracle's k-ordered
+// fmaf chain).  B rows past d are clamped to row d - 1: their A entries are 0
+// and fma(0, b, acc) == acc for every finite b (acc is never -0).  B rows are
+// streamed from global in chunks of KS k-steps, two chunks in flight.
+template <int NT = NTL, int KS = 8>
+__device__ __forceinline__ void coarse_key_tile(f4 (&acc)[NT], const float* xs, int lda, int arow0,
+                                                const float* __restrict__ centT, int ldc, int nlist, int d, int dk,
+                                                int c0, int lane) {
+  static_assert(64 % (8 * KS) == 0, "dk is padded to 64");
+#pragma unroll
+  for (int t = 0; t < NT; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  const int i16 = lane & 15, k4 = lane >> 4;
+  const float* bcol[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) bcol[t] = centT + min(c0 + t * 16 + i16, nlist - 1);  // clamped columns
+  float b0[KS][NT], b1[KS][NT];
+  auto load_b = [&](int k0, float (&b)[KS][NT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < KS; j++) {
+      const int64_t kr = min(k0 + 4 * j + k4, d - 1);
+#pragma unroll
+      for (int t = 0; t < NT; t++) b[j][t] = bcol[t][kr * ldc];
+    }
+  };
+  auto mma = [&](int k0, const float (&b)[KS][NT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < KS; j++) {
+      const float av = xs[(k0 + 4 * j + k4) * lda + arow0 + i16];
+#pragma unroll
+      for (int t = 0; t < NT; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
+    }
+  };
+  constexpr int CH = 4 * KS;  // k per chunk
+  load_b(0, b0);
+  for (int k0 = 0; k0 < dk; k0 += 2 * CH) {
+    load_b(k0 + CH, b1);
+    mma(k0, b0);
+    load_b(k0 + 2 * CH, b0);  // past the end on the last pass: clamped, unused
+    mma(k0 + CH, b1);
+  }
+}
+
+// the quantizer key from <x, c>: L2 max(0, (|x|^2 + |c|^2) - 2 <x, c>), IP -<x, c>
+__device__ __forceinline__ float coarse_key(float dot, float xn, float cn, int ip) {
+  if (ip) return -dot;
+  const float v = (xn + cn) - 2.0f * dot;
+  return v < 0.f ? 0.f : v;
+}
+
 __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
                                                      const float* __restrict__ centT, int ldc,
                                                      const float* __restrict__ cn, int nlist,
@@ -770,71 +857,13 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   const int dk = (d + 63) & ~63;  // A rows, zero-padded to whole double chunks
   float* xs = g_lds;              // [dk][GQ]: the A operand, k-major
   float* xn = xs + dk * GQ;       // [GQ]
-  fill_cols(xs, x, q0, nq, d, dk, tid);
-  __syncthreads();
+  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
   CDIAG(1);
-  // |x_q|^2 in Faiss tree order: with d % 8 == 0 the 8 lane sums of each query
-  // are 8 independent sequential chains (threads i * 8 + j), folded by 16 threads
-  float* a8 = xn + GQ;  // [GQ][8]
-  if (d % 8 == 0) {
-    if (tid < GQ * 8) {
-      const int i = tid >> 3, j = tid & 7;
-      float acc8 = 0.f;
-      for (int k = j; k < d; k += 8) {
-        const float v = xs[k * GQ + i];
-        acc8 = acc8 + v * v;
-      }
-      a8[i * 8 + j] = acc8;
-    }
-    __syncthreads();
-    if (tid < GQ) {
-      const float* r = a8 + tid * 8;
-      const float h0 = (r[4] + r[0]) + (r[5] + r[1]);
-      const float h1 = (r[6] + r[2]) + (r[7] + r[3]);
-      xn[tid] = h0 + h1;
-    }
-  } else if (tid < GQ) {
-    xn[tid] = tree<K_NORM>([&](int t) { return xs[t * GQ + tid]; }, [&](int t) { return xs[t * GQ + tid]; }, d);
-  }
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  constexpr int NTL = GC / 64;  // 16 x 16 tiles per wave
   f4 acc[NTL];
-#pragma unroll
-  for (int t = 0; t < NTL; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  const int i16 = lane & 15, k4 = lane >> 4;
-  const float* bcol[NTL];
-#pragma unroll
-  for (int t = 0; t < NTL; t++) bcol[t] = centT + min(c0 + t * 16 + i16, nlist - 1);  // clamped columns
-  // B operand rows, 8 k-steps (32 k) per chunk, two chunks in flight.  Rows
-  // past d are clamped to row d - 1: their A entries are 0 and fma(0, b, acc)
-  // == acc for every finite b (acc is never -0).
-  constexpr int KS = 8;
-  float b0[KS][NTL], b1[KS][NTL];
-  auto load_b = [&](int k0, float (&b)[KS][NTL]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < KS; j++) {
-      const int64_t kr = min(k0 + 4 * j + k4, d - 1);
-#pragma unroll
-      for (int t = 0; t < NTL; t++) b[j][t] = bcol[t][kr * ldc];
-    }
-  };
-  auto mma = [&](int k0, const float (&b)[KS][NTL]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < KS; j++) {
-      const float av = xs[(k0 + 4 * j + k4) * GQ + i16];
-#pragma unroll
-      for (int t = 0; t < NTL; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
-    }
-  };
-  load_b(0, b0);
-  for (int k0 = 0; k0 < dk; k0 += 64) {
-    load_b(k0 + 32, b1);
-    mma(k0, b0);
-    load_b(k0 + 64, b0);  // past the end on the last pass: clamped, unused
-    mma(k0 + 32, b1);
-  }
+  coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
   CDIAG(2);
   __syncthreads();  // xn
+  const int i16 = lane & 15, k4 = lane >> 4;
 #pragma unroll
   for (int t = 0; t < NTL; t++) {
     const int c = c0 + t * 16 + i16;
@@ -844,20 +873,46 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     for (int r = 0; r < 4; r++) {
       const int i = k4 * 4 + r;
       if (q0 + i >= nq) continue;
-      float v;
-      if (ip) {
-        v = -acc[t][r];
-      } else {
-        v = (xn[i] + cnv) - 2.0f * acc[t][r];
-        if (v < 0.f) v = 0.f;
-      }
-      keys[(q0 + i) * nlist + c] = v;
+      keys[(q0 + i) * nlist + c] = coarse_key(acc[t][r], xn[i], cnv, ip);
     }
   }
 #ifdef DIAG_CSTAMPS
   __builtin_amdgcn_s_waitcnt(0);
 #endif
   CDIAG(5);
+}
+
+// Write a query's top-nprobe (run: packed (key, list), ascending across the
+// wave) and, with cp.on, plan its probes for the list-major scan.
+__device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, int nprobe, float* __restrict__ out_dis,
+                                            int64_t* __restrict__ out_list, int ip, const float* __restrict__ x, int d,
+                                            const CoarsePlan& cp) {
+  const bool empty = run == kKcNone;
+  const float rd = kc_key(run);
+  const int64_t ri = empty ? kSentinelId : (int64_t)(uint32_t)run;
+  if (lane < nprobe) {
+    out_dis[q * nprobe + lane] = empty ? (ip ? -FLT_MAX : FLT_MAX) : (ip ? -rd : rd);
+    out_list[q * nprobe + lane] = empty ? -1 : ri;
+  }
+  if (cp.on) {  // list-major planning of this query's probes (k_plan_count's rules)
+    const int64_t l = ri;  // kSentinelId when empty: outside [lo, hi)
+    const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
+    const uint64_t um = __ballot(use);
+    const int fp = um ? (int)__builtin_ctzll(um) : 64;
+    if (lane == 0) {
+      cp.pl.tauq[q] = f2ord(kInf);
+      cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
+    }
+    if (use) {
+      float d0 = rd;
+      if (ip) {
+        const float* xq = x + q * d;
+        const float* cl = cp.cent + l * d;
+        d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
+      }
+      plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
+    }
+  }
 }
 
 // Per query (one wave): the nprobe (<= 64) smallest keys of its row, by
@@ -925,32 +980,7 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
     __builtin_amdgcn_wave_barrier();  // scratch reuse
   }
   SDIAG(3);
-  const bool empty = run == kKcNone;
-  const float rd = kc_key(run);
-  const int64_t ri = empty ? kSentinelId : (int64_t)(uint32_t)run;
-  if (lane < nprobe) {
-    out_dis[q * nprobe + lane] = empty ? (ip ? -FLT_MAX : FLT_MAX) : (ip ? -rd : rd);
-    out_list[q * nprobe + lane] = empty ? -1 : ri;
-  }
-  if (cp.on) {  // list-major planning of this query's probes (k_plan_count's rules)
-    const int64_t l = ri;  // kSentinelId when empty: outside [lo, hi)
-    const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
-    const uint64_t um = __ballot(use);
-    const int fp = um ? (int)__builtin_ctzll(um) : 64;
-    if (lane == 0) {
-      cp.pl.tauq[q] = f2ord(kInf);
-      cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
-    }
-    if (use) {
-      float d0 = rd;
-      if (ip) {
-        const float* xq = x + q * d;
-        const float* cl = cp.cent + l * d;
-        d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
-      }
-      plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
-    }
-  }
+  coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
 #ifdef DIAG_CSTAMPS
   __builtin_amdgcn_s_waitcnt(0);
 #endif
@@ -1948,6 +1978,105 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   }
 }
 
+// ------------------------------------------- large-nlist coarse (no key matrix)
+// Segmented coarse quantizer: workgroup = 16 queries x one segment of `seg`
+// centroids, walked in key tiles of 128 (coarse_key_tile: the MFMA keys of
+// k_coarse_gemm).  Each tile's keys go through LDS; wave w keeps the nprobe best
+// (key, list) words of queries 4w .. 4w + 3 in a packed one-row top-k, into
+// which a tile's candidates under its nprobe-th are inserted one by one when
+// few, bulk-merged when many.  Output: cand [nq][nseg][nprobe] packed words
+// (kKcNone = none).  The [nq][nlist] key matrix is never written (C4: 1024 x
+// 65536 keys would be 256 MB per chunk).
+__global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__ x, int64_t nq, int d,
+                                                       const float* __restrict__ centT, int ldc,
+                                                       const float* __restrict__ cn, int nlist, int ip, int seg,
+                                                       int nseg, int nprobe, uint64_t* __restrict__ cand) {
+  extern __shared__ __attribute__((aligned(16))) float g_lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t q0 = (int64_t)(blockIdx.x / nseg) * GQ;
+  const int sg = blockIdx.x % nseg;
+  const int cb = sg * seg, ce = min(nlist, cb + seg);
+  const int dk = (d + 63) & ~63;
+  float* xs = g_lds;             // [dk][GQ]
+  float* xn = xs + dk * GQ;      // [GQ] + 128 scratch
+  float* kt = xn + GQ + GQ * 8;  // [GQ][GC] key tile
+  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+  const int i16 = lane & 15, k4 = lane >> 4;
+  PackedTopK<1> tk[4];  // queries 4 wave .. 4 wave + 3
+#pragma unroll
+  for (int u = 0; u < 4; u++) tk[u].init(nprobe);
+  for (int t0 = cb; t0 < ce; t0 += GC) {
+    f4 acc[NTL];
+    coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, t0 + wave * 32, lane);
+    __syncthreads();  // xn (first tile); the previous tile's keys have been read
+#pragma unroll
+    for (int t = 0; t < NTL; t++) {
+      const int c = t0 + wave * 32 + t * 16 + i16;
+      const float cnv = ip ? 0.f : cn[min(c, nlist - 1)];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = k4 * 4 + r;
+        kt[i * GC + wave * 32 + t * 16 + i16] = coarse_key(acc[t][r], xn[i], cnv, ip);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = wave * 4 + u;
+#pragma unroll
+      for (int h = 0; h < GC / 64; h++) {
+        const int c = t0 + h * 64 + lane;
+        const uint64_t p = c < ce ? pack_kc(kt[i * GC + h * 64 + lane], c) : kKcNone;
+        const bool pass = p < tk[u].tp;
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+        if (!mk) continue;  // wave-uniform
+        if (__popcll(mk) > 4)
+          kc_bulk_merge(tk[u], pass ? p : kKcNone, lane);
+        else
+          tk[u].insert(mk, p, lane);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int64_t q = q0 + wave * 4 + u;
+    if (q < nq && lane < nprobe) cand[(q * nseg + sg) * nprobe + lane] = tk[u].p[0];
+  }
+}
+
+// Per query (one wave): merge its nseg x nprobe segment candidates into the
+// final top-nprobe by (key, list), then emit and plan as k_coarse_select does.
+__global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __restrict__ cand, int64_t nq, int nseg,
+                                                            int nprobe, float* __restrict__ out_dis,
+                                                            int64_t* __restrict__ out_list, int ip,
+                                                            const float* __restrict__ x, int d, CoarsePlan cp) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;  // wave-uniform
+  const int total = nseg * nprobe;
+  const uint64_t* row = cand + q * total;
+  uint64_t run = kKcNone;
+  for (int b0 = 0; b0 < total; b0 += 256) {
+    uint64_t p[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int e = b0 + u * 64 + lane;
+      p[u] = e < total ? row[e] : kKcNone;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint64_t tp = readlane_u64(run, nprobe - 1);
+      if (__builtin_amdgcn_ballot_w64(p[u] < tp)) {
+        kc_sort64(p[u], lane);
+        kc_merge64(run, p[u], lane);
+      }
+    }
+  }
+  coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
+}
+
 // Per query (one wave): merge the per-wave partial lists of every scanned
 // probe ([probe][4 waves][k], sorted by (key, position)).  All entries are
 // fetched in batches of 64 lanes x B loads (one round trip per batch); labels
@@ -2353,6 +2482,48 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
   }
   hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
                      (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
+}
+
+int coarse_segments(int64_t nq, int nlist) {
+  const int64_t qt = (nq + GQ - 1) / GQ;
+  const int tiles = (nlist + GC - 1) / GC;
+  const int want = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (1024 + qt - 1) / qt));  // >= 1024 workgroups
+  const int seg = (tiles + want - 1) / want * GC;
+  return (nlist + seg - 1) / seg;
+}
+
+void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
+                             int nprobe, uint64_t* cand, float* out_dis, int64_t* out_list, hipStream_t s, bool ip,
+                             const ListPlan* plan, const int64_t* list_off, int lo, int hi, const float* cent) {
+  if (nq <= 0) return;
+  const int nseg = coarse_segments(nq, nlist);
+  const int tiles = (nlist + GC - 1) / GC;
+  const int seg = (tiles + nseg - 1) / nseg * GC;
+  const int dk = (d + 63) & ~63;
+  const size_t smem = sizeof(float) * ((size_t)dk * GQ + GQ + GQ * 8 + GQ * GC);
+  if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device
+    static uint64_t attr_done = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 64 && !(attr_done & (1ull << dev))) {
+      (void)hipFuncSetAttribute((const void*)k_coarse_segtop, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr_done |= 1ull << dev;
+    }
+  }
+  const unsigned grid = (unsigned)(nblocks(nq, GQ) * (unsigned)nseg);
+  hipLaunchKernelGGL(k_coarse_segtop, dim3(grid), dim3(256), smem, s, x, nq, d, centT, (nlist + 3) & ~3, cn, nlist,
+                     ip ? 1 : 0, seg, nseg, nprobe, cand);
+  CoarsePlan cp;
+  if (plan) {
+    cp.pl = *plan;
+    cp.on = 1;
+    cp.list_off = list_off;
+    cp.lo = lo;
+    cp.hi = hi;
+    cp.cent = cent;
+  }
+  hipLaunchKernelGGL(k_coarse_select_cand, dim3(nblocks(nq, 4)), dim3(256), 0, s, cand, nq, nseg, nprobe, out_dis,
+                     out_list, ip ? 1 : 0, x, d, cp);
 }
 
 void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, float* out_dis, int64_t* out_list,

@@ -245,3 +245,24 @@ def test_sliced_coarse_allgather_shards_c2(sift1m, nshards):
     torch.cuda.synchronize()
     Dr, Ir = ox.search(xq, 10)
     assert_same(torch.cat(Dm).cpu().numpy(), torch.cat(Im).cpu().numpy(), Dr, Ir)
+
+
+@pytest.mark.parametrize("nq,nprobe", [(1, 1), (17, 33), (1000, 64)])
+def test_segmented_coarse_matches_oracle(nq, nprobe):
+    """nlist >= 8192 takes the segmented coarse quantizer (per-segment top-nprobe
+    on the matrix cores, no [nq][nlist] key matrix); nlist = 20000 leaves a
+    partial last tile, and the batch sizes give 1 to many segments per query."""
+    import torch
+
+    rng = np.random.default_rng(7)
+    d, nlist, M = 96, 20000, 48
+    cent = rng.integers(0, 64, size=(nlist, d)).astype(np.float32)
+    cent[123] = cent[456]  # an exact tie: ordered by list id
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+    ix.set_trained(cent, rng.standard_normal((M, 256, d // M), dtype=np.float32))
+    ix.nprobe = nprobe
+    xq = rng.integers(0, 64, size=(nq, d)).astype(np.float32)
+    Dq, Iq = ix.coarse_device(torch.from_numpy(xq).cuda())
+    Dr, Ir = O.coarse_search(xq, cent, nprobe)
+    np.testing.assert_array_equal(Iq.cpu().numpy(), Ir)
+    np.testing.assert_array_equal(Dq.cpu().numpy(), Dr)

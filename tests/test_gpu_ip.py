@@ -173,7 +173,7 @@ def test_ip_shards_merge(c3_ip):
 
 
 def test_ip_large_nlist_split_coarse():
-    """nlist > 8192: the coarse key matrix + row select, then k_plan_count."""
+    """nlist >= 8192 (not a multiple of the 128-centroid tile): the segmented coarse quantizer."""
     xt = datasets.synthetic_sift_like(12_000, 32, seed=4321, n_centres=5000)
     xb = datasets.synthetic_sift_like(60_000, 32, seed=1234, n_centres=5000)
     xq = datasets.synthetic_sift_like(40, 32, seed=123, n_centres=5000)
