@@ -2057,7 +2057,8 @@ __global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __re
   if (q >= nq) return;  // wave-uniform
   const int total = nseg * nprobe;
   const uint64_t* row = cand + q * total;
-  uint64_t run = kKcNone;
+  PackedTopK<1> tk;
+  tk.init(nprobe);
   for (int b0 = 0; b0 < total; b0 += 256) {
     uint64_t p[4];
 #pragma unroll
@@ -2067,14 +2068,16 @@ __global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __re
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const uint64_t tp = readlane_u64(run, nprobe - 1);
-      if (__builtin_amdgcn_ballot_w64(p[u] < tp)) {
-        kc_sort64(p[u], lane);
-        kc_merge64(run, p[u], lane);
-      }
+      const bool pass = p[u] < tk.tp;
+      const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+      if (!mk) continue;  // wave-uniform
+      if (__popcll(mk) > 4)
+        kc_bulk_merge(tk, pass ? p[u] : kKcNone, lane);
+      else
+        tk.insert(mk, p[u], lane);
     }
   }
-  coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
+  coarse_emit(tk.p[0], q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
 }
 
 // Per query (one wave): merge the per-wave partial lists of every scanned
