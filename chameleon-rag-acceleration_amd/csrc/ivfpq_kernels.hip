@@ -1217,6 +1217,7 @@ __device__ __forceinline__ void write_item(const ListPlan& pl, const int64_t* __
   rp[3] = make_int4(r[12], r[13], r[14], r[15]);
 }
 
+#ifdef PLAN_MIX_KINDS  // A/B planning variant (r02: within noise at C2)
 // The items of one list when its first-probe pairs (kind 0: c0 of them) and
 // other pairs (c1) share items: slots 0..c-1 run over the kind-0 bucket, then
 // the kind-1 bucket.  The first ceil(c0 / G) items (every first-probe pair, the
@@ -1254,6 +1255,7 @@ __device__ __forceinline__ void write_item_mixed(const ListPlan& pl, const int64
   rp[2] = make_int4(r[8], r[9], r[10], r[11]);
   rp[3] = make_int4(r[12], r[13], r[14], r[15]);
 }
+#endif
 
 __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
                                                              int nloc, int G) {
