@@ -135,7 +135,8 @@ void kmeans_update(const float* x, int64_t n, int d, int k, const int64_t* assig
   }
 }
 
-constexpr size_t kChunkBytes = size_t(256) << 20;  // bound for [rows][cols] fp32 scratch
+constexpr size_t kChunkBytes = size_t(256) << 20;    // bound for [rows][cols] fp32 scratch
+constexpr size_t kPartialBytes = size_t(2048) << 20;  // bound for a chunk's per-wave partial top-k lists
 constexpr int kSegmentedNlist = 8192;  // from this nlist on, the coarse quantizer never writes the key matrix
 
 }  // namespace
@@ -465,8 +466,13 @@ struct ivfpq_index {
     order_after_last(s);
     const int np = preassigned ? nprobe : eff_nprobe();
     const int nloc = std::max(list_hi - list_lo, 1);
-    const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)np * k * 48, (size_t)nloc * 16});
-    const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / per_q));
+    // queries per chunk: [c][nlist] keys, T3 and buckets within kChunkBytes; the
+    // per-wave partial lists ([c][np][4][k] keys + positions, 48 B per entry and
+    // query) within kPartialBytes, so large k still runs whole 1024-query batches
+    // (C3, k = 1000, nprobe 32: 1.5 MB per query)
+    const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)nloc * 16});
+    const int64_t qc = std::max<int64_t>(
+        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * k * 48))}));
     w_T3.ensure(sizeof(float) * qc * M * ksub);
     if (!preassigned) {
       w_lists.ensure(sizeof(int64_t) * qc * np);
