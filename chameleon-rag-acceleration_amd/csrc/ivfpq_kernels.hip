@@ -2332,12 +2332,17 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       }
     }
   }
+  // Full merge.  For k > 64 the entries are visited rank-major across the
+  // L = 4 nprobe sorted lists (every list's entry i, then every list's entry
+  // i + 1, ...), so the running k-th key falls fast and few labels are looked
+  // up; once a batch of at least L consecutive entries (one per list) admits
+  // nothing, no later entry of any list can (each list is ascending and the
+  // k-th key only falls).
   WaveTopK<R> tk;
   tk.init(k);
-  const int per_probe = 4 * k;
-  const int total = np * per_probe;
-  const float* pd = pl.partD + q * (int64_t)total;
-  const int64_t* pi = pl.partI + q * (int64_t)total;
+  const int L = 4 * np;
+  const int total = L * k;
+  const int64_t qbase = q * (int64_t)total;
   for (int e0 = 0; e0 < total; e0 += 64 * B) {
     float d[B];
     int64_t pos[B];
@@ -2347,7 +2352,10 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       d[b] = kInf;
       pos[b] = -1;
       if (e < total) {
-        const int p = e / per_probe;
+        // R == 1 (k <= 64, a fast-path miss): list-major order; R >= 2: rank-major
+        const int i = R == 1 ? e % k : e / L;
+        const int j = R == 1 ? e / k : e - (e / L) * L;  // rank i of list j = (probe j / 4, wave j % 4)
+        const int p = j >> 2;
         bool scanned;
         if (np <= 64) {
           scanned = (pl.qmask[q] >> p) & 1;
@@ -2356,11 +2364,16 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
           scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
         }
         if (scanned) {
-          d[b] = pd[e];
-          pos[b] = pi[e];
+          const int64_t at = qbase + (int64_t)j * k + i;
+          d[b] = pl.partD[at];
+          pos[b] = pl.partI[at];
         }
       }
     }
+    bool any = false;
+#pragma unroll
+    for (int b = 0; b < B; b++) any = any || (pos[b] >= 0 && d[b] <= tk.td);
+    if (R >= 2 && L <= 64 * B && __builtin_amdgcn_ballot_w64(any) == 0) break;  // wave-uniform
 #pragma unroll
     for (int b = 0; b < B; b++) {
       const bool maybe = pos[b] >= 0 && d[b] <= tk.td;
