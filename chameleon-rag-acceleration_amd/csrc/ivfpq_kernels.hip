@@ -2665,7 +2665,7 @@ template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
 #ifndef SCAN_JB16
-#define SCAN_JB16 8  // A/B builds may lower it
+#define SCAN_JB16 6  // r02 A/B at C2: 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
 #endif
   constexpr int JB = M <= 16 ? SCAN_JB16 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs), even
   if (ev) (void)hipEventRecord(ev[0], s);
