@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -99,6 +100,21 @@ std::vector<int64_t> rand_perm_prefix(int64_t n, int64_t k, uint64_t seed) {
     out[i] = p[i];
   }
   return out;
+}
+
+// Spherical k-means step (Faiss Clustering with spherical = true, which IndexIVF
+// sets for METRIC_INNER_PRODUCT; fvec_renorm_L2): every centroid scaled to unit
+// L2 norm.  Same arithmetic as or_renorm_rows in oracle/ivfpq_oracle.c.
+void renorm_rows(float* x, int64_t n, int d) {
+  for (int64_t i = 0; i < n; i++) {
+    float* xi = x + i * d;
+    float nr = 0.f;
+    for (int t = 0; t < d; t++) nr += xi[t] * xi[t];
+    if (nr > 0.f) {
+      const float inv = (float)(1.0 / (double)sqrtf(nr));
+      for (int t = 0; t < d; t++) xi[t] *= inv;
+    }
+  }
 }
 
 void kmeans_update(const float* x, int64_t n, int d, int k, const int64_t* assign, float* cent) {
@@ -314,6 +330,7 @@ struct ivfpq_index {
                         std::to_string(k) + ")");
     const auto init = rand_perm_prefix(n, k, seed);
     for (int c = 0; c < k; c++) std::memcpy(cent + (size_t)c * dd, x + init[c] * dd, sizeof(float) * dd);
+    if (ip_assign) renorm_rows(cent, k, dd);  // spherical: unit-norm centroids (Faiss post_process_centroids)
     // keep the whole training set resident when it fits the scratch bound
     DevBuf xall;
     const bool resident = (size_t)n * dd * 4 <= (size_t(2) << 30);
@@ -330,6 +347,7 @@ struct ivfpq_index {
       assign_top1(x, n, dd, w_cent.as<float>(), w_cn.as<float>(), k, assign.data(),
                   resident ? xall.as<float>() : nullptr, ip_assign);
       kmeans_update(x, n, dd, k, assign.data(), cent);
+      if (ip_assign) renorm_rows(cent, k, dd);
     }
   }
 
@@ -369,6 +387,8 @@ struct ivfpq_index {
     // Device image: each list sorted by label (stable).  Results do not depend
     // on the order inside a list, and label-sorted lists let the scan kernels
     // rank candidates by code position instead of loading labels.
+    // (M = 16: each code rotated by its list position, see codes_rotated)
+    const bool rot = codes_rotated(M);
     std::vector<int64_t> perm;
     for (int l = 0; l < nlist; l++) {
       const int64_t n = (int64_t)lids[l].size();
@@ -378,7 +398,12 @@ struct ivfpq_index {
       const int64_t* lid = lids[l].data();
       std::stable_sort(perm.begin(), perm.end(), [lid](int64_t a, int64_t b) { return lid[a] < lid[b]; });
       for (int64_t i = 0; i < n; i++) {
-        std::memcpy(codes.data() + (off[l] + i) * M, lcodes[l].data() + perm[i] * M, M);
+        uint8_t* dst = codes.data() + (off[l] + i) * M;
+        const uint8_t* src = lcodes[l].data() + perm[i] * M;
+        if (rot)
+          for (int m = 0; m < M; m++) dst[(m + i) & 15] = src[m];
+        else
+          std::memcpy(dst, src, M);
         ids[off[l] + i] = lid[perm[i]];
       }
     }

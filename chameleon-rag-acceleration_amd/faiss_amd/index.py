@@ -404,9 +404,18 @@ class IndexIVFPQ:
         if not ans.flags.writeable:
             raise RuntimeError("answer buffer must be writable")
         ln = ctypes.c_int64(0)
-        _lib.check(_lib.load().ivfpq_serve_request(self._h, _ptr(buf, _lib.c_u8p), buf.size, int(bool(with_lists)),
-                                                   int(batch_size), int(dim), np_, _ptr(ans, _lib.c_u8p), ans.size,
-                                                   ctypes.byref(ln)))
+        # a plain request is searched with the index's nprobe: an explicit nprobe
+        # applies for this call only (with lists, it is the request's column count)
+        saved = self.nprobe
+        if not with_lists and nprobe is not None:
+            self.nprobe = np_
+        try:
+            _lib.check(_lib.load().ivfpq_serve_request(self._h, _ptr(buf, _lib.c_u8p), buf.size,
+                                                       int(bool(with_lists)), int(batch_size), int(dim), np_,
+                                                       _ptr(ans, _lib.c_u8p), ans.size, ctypes.byref(ln)))
+        finally:
+            if self.nprobe != saved:
+                self.nprobe = saved
         return out if len(out) == ln.value else memoryview(out)[:ln.value]
 
     # ------------------------------------------------------------ stage timing

@@ -100,8 +100,23 @@ class LinearTransform:
             raise RuntimeError(f"apply_device: x must be a float32 CUDA tensor [n, {self.d_in}]")
         x = x.contiguous()
         AT, b = self._device_mats(x.device.index)
-        y = torch.empty((x.shape[0], self.d_out), dtype=torch.float32, device=x.device)
-        s = stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
+        cur = torch.cuda.current_stream(x.device)
+        if stream is None or int(stream) == cur.cuda_stream:
+            y = torch.empty((x.shape[0], self.d_out), dtype=torch.float32, device=x.device)
+            s = cur.cuda_stream
+        else:
+            # a caller's stream: it waits for the current stream (x's producer, the
+            # copies of AT and b), and y is allocated on it (the caching allocator
+            # then never hands y's block to the current stream while it is in use);
+            # x, AT and b are marked as used by it
+            ext = torch.cuda.ExternalStream(int(stream), device=x.device)
+            ext.wait_stream(cur)
+            with torch.cuda.stream(ext):
+                y = torch.empty((x.shape[0], self.d_out), dtype=torch.float32, device=x.device)
+            for t in (x, AT, b):
+                if t is not None:
+                    t.record_stream(ext)
+            s = int(stream)
         _lib.check(_lib.load().ivfpq_linear_transform_device(
             x.shape[0], self.d_in, self.d_out, AT.data_ptr(), b.data_ptr() if b is not None else None,
             x.data_ptr(), y.data_ptr(), ctypes.c_void_p(s)))
@@ -258,6 +273,41 @@ class IndexPreTransform:
 
     def search_device(self, x, k, D=None, I=None, stream=None):
         return self.index.search_device(self.apply_chain_device(x, stream), k, D, I, stream)
+
+    # the rest of the IVF-PQ surface callers reach through an OPQ index
+    # (faiss_server.py / faiss_retriever.py: coarse step, preassigned search, wire requests)
+    def coarse_device(self, x, Iq=None, Dq=None, stream=None):
+        return self.index.coarse_device(self.apply_chain_device(x, stream), Iq, Dq, stream)
+
+    def search_preassigned_device(self, x, k, Iq, Dq=None, D=None, I=None, stream=None):
+        return self.index.search_preassigned_device(self.apply_chain_device(x, stream), k, Iq, Dq, D, I, stream)
+
+    def search_preassigned(self, *args):
+        """Both forms of IndexIVFPQ.search_preassigned, on the transformed queries."""
+        if len(args) >= 7:
+            n, x, k, Iq, Dq, D, I = args[:7]
+            xt = self.apply_chain(np.ascontiguousarray(x, np.float32).reshape(-1, self.d))
+            return self.index.search_preassigned(n, xt, k, Iq, Dq, D, I, *args[7:])
+        x, k, Iq = args[:3]
+        xt = self.apply_chain(np.ascontiguousarray(x, np.float32).reshape(-1, self.d))
+        return self.index.search_preassigned(xt, k, Iq, *args[3:])
+
+    def serve_request(self, msg, batch_size, dim, with_lists=False, nprobe=None, out=None):
+        """A wire request on the pre-transform dimension: the queries are decoded,
+        transformed on the GPU and re-encoded for the wrapped index."""
+        from . import wire
+
+        if dim != self.d:
+            raise RuntimeError(f"dim={dim} does not match the index (d={self.d})")
+        np_ = int(self.index.nprobe if nprobe is None else nprobe)
+        if with_lists:
+            k, q, lists = wire.decode_request_with_lists(msg, batch_size, dim, np_)
+            msg2 = wire.encode_request_with_lists(self.apply_chain(np.array(q)), lists, batch_size, self.index.d,
+                                                  np_, k)
+        else:
+            k, q = wire.decode_request(msg, batch_size, dim)
+            msg2 = wire.encode_request(self.apply_chain(np.array(q)), k, batch_size, self.index.d)
+        return self.index.serve_request(msg2, batch_size, self.index.d, with_lists=with_lists, nprobe=nprobe, out=out)
 
     def reset(self):
         self.index.reset()

@@ -446,8 +446,25 @@ void or_kmeans_update(const float *x, int64_t n, int d, int k, const int64_t *as
     free(cnt);
 }
 
+/* Spherical step (Faiss Clustering::spherical, set by IndexIVF for
+ * METRIC_INNER_PRODUCT; fvec_renorm_L2): each row scaled to unit L2 norm,
+ * inv = 1.0 / sqrtf(|x|^2) as Faiss computes it.  Sequential float norm (the same
+ * code as renorm_rows in csrc/ivfpq_index.cpp). */
+void or_renorm_rows(float *x, int64_t n, int d) {
+    for (int64_t i = 0; i < n; i++) {
+        float *xi = x + i * d;
+        float nr = 0.f;
+        for (int t = 0; t < d; t++) nr += xi[t] * xi[t];
+        if (nr > 0.f) {
+            const float inv = (float)(1.0 / (double)sqrtf(nr));
+            for (int t = 0; t < d; t++) xi[t] *= inv;
+        }
+    }
+}
+
 /* Lloyd k-means, niter rounds of (assign: first nearest centroid by coarse
- * distance, or for IP (metric 0) first largest inner product; update). */
+ * distance, or for IP (metric 0) first largest inner product; update).  IP is
+ * spherical: centroids renormalized after the initialization and every update. */
 void or_kmeans_metric(const float *x, int64_t n, int d, int k, int niter, uint64_t seed, float *cent, int nthreads,
                       int metric) {
     const int ip = metric == 0;
@@ -455,6 +472,7 @@ void or_kmeans_metric(const float *x, int64_t n, int d, int k, int niter, uint64
     or_rand_perm_prefix(n, k, seed, init);
     for (int c = 0; c < k; c++) memcpy(cent + (int64_t)c * d, x + init[c] * d, sizeof(float) * d);
     free(init);
+    if (ip) or_renorm_rows(cent, k, d);
     int64_t *assign = (int64_t *)malloc(sizeof(int64_t) * n);
     float *cn = (float *)malloc(sizeof(float) * k);
     for (int it = 0; it < niter; it++) {
@@ -466,6 +484,7 @@ void or_kmeans_metric(const float *x, int64_t n, int d, int k, int niter, uint64
             assign[i] = or_assign(xi, xn, cent, cn, k, d, ip);
         }
         or_kmeans_update(x, n, d, k, assign, cent);
+        if (ip) or_renorm_rows(cent, k, d);
     }
     free(assign);
     free(cn);

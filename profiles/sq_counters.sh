@@ -23,7 +23,7 @@ acc = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/g*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         kn = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("chivf::", "")
-    acc[(kn[:40], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        acc[(kn[:40], r["Counter_Name"])].append(float(r["Counter_Value"]))
 for k in sorted(acc):
     v = acc[k]
     print(f"{k[0]:40s} {k[1]:28s} n={len(v):3d} mean={sum(v)/len(v):14.1f}")

@@ -217,3 +217,22 @@ def test_ip_train_and_add_match_oracle():
     D, I = ix.search(x[3000:3100], 10)
     Dr, Ir = ox.search(x[3000:3100], 10)
     assert_same(D, I, Dr, Ir)
+
+
+@pytest.mark.gpu
+def test_ip_train_spherical_on_raw_data_matches_oracle():
+    """IP training on raw non-negative rows (no centring): the GPU k-means is
+    spherical like Faiss's (unit-norm centroids), equal to the oracle's bit for
+    bit, and the lists stay balanced."""
+    x = datasets.synthetic_sift_like(8000, 32, seed=11, n_centres=40)
+    ix = faiss.IndexIVFPQ(None, 32, 32, 8, 8, IP, device=0)
+    ix.niter_coarse, ix.niter_pq, ix.seed = 8, 4, 5
+    ix.train(x)
+    ox = O.OracleIVFPQ(32, 32, 8, metric=O.METRIC_INNER_PRODUCT)
+    ox.train(x, niter_coarse=8, niter_pq=4, seed=5)
+    np.testing.assert_array_equal(ix.centroids(), ox.centroids)
+    np.testing.assert_array_equal(ix.codebook(), ox.codebook)
+    np.testing.assert_allclose(np.linalg.norm(ix.centroids().astype(np.float64), axis=1), 1.0, rtol=1e-5)
+    ix.add(x)
+    sizes = ix.invlists.list_sizes()
+    assert sizes.max() < 0.25 * len(x), sizes

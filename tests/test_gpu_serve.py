@@ -124,3 +124,19 @@ def test_serve_rejects_malformed_requests(golden_dir):
     ans = ix.serve_request(bytes(msg), b, dim)
     D, I = ix.search(xq, 10)
     assert bytes(ans) == bytes(wire.encode_answer(I, D, 10, b))
+
+
+def test_serve_plain_request_honors_nprobe_argument(golden_dir):
+    """serve_request(nprobe=p) on a plain request searches with p probes for that
+    call only; the index's own nprobe is restored afterwards."""
+    ix, ox, z = golden_pair(golden_dir)
+    xq = np.ascontiguousarray(z["xq"][:8], np.float32)
+    b, dim = xq.shape
+    p = int(z["nprobe"])
+    ix.nprobe = 1
+    ox.nprobe = p
+    msg = wire.encode_request(xq, 10, b, dim)
+    ans = ix.serve_request(msg, b, dim, nprobe=p)
+    Dr, Ir = ox.search(xq, 10)
+    assert bytes(ans) == bytes(wire.encode_answer(Ir, Dr, 10, b))
+    assert ix.nprobe == 1

@@ -82,3 +82,58 @@ def test_opq_index_matches_oracle(tmp_path):
     D2, I2 = back.search(xq, k)
     np.testing.assert_array_equal(I2, I)
     np.testing.assert_array_equal(D2, D)
+
+
+def test_opq_index_full_surface():
+    """An "OPQ..,IVF..,PQ.." index behind the rest of the surface: preassigned
+    search (both forms), the coarse step on the device, a wire request through
+    RetrievalService (plain and with lists) -- each equal to transforming the
+    queries by hand and asking the wrapped IVF-PQ -- and the apply on a side
+    stream equal to the apply on the current stream."""
+    import torch
+
+    from faiss_amd import wire
+    from faiss_amd.server import RetrievalService
+
+    d = 32
+    xt = datasets.synthetic_sift_like(4000, d, seed=21, n_centres=100)
+    xb = datasets.synthetic_sift_like(8000, d, seed=22, n_centres=100)
+    xq = datasets.synthetic_sift_like(16, d, seed=23, n_centres=100)
+    ix = faiss.index_factory(d, "OPQ4,IVF32,PQ4")
+    ix.chain[0].niter = 2
+    ix.train(xt)
+    ix.add(xb)
+    ix.nprobe = 4
+    ivf = faiss.downcast_index(ix.index)
+    xqt = ix.apply_chain(xq)
+    k = 5
+    Dref, Iref = ivf.search(xqt, k)
+    D, I = ix.search(xq, k)
+    np.testing.assert_array_equal(I, Iref)
+    Iq = torch.empty((16, 4), dtype=torch.int64, device="cuda")
+    Dq = torch.empty((16, 4), dtype=torch.float32, device="cuda")
+    ix.coarse_device(torch.from_numpy(xq).cuda(), Iq, Dq)
+    Dq2, Iq2 = ivf.coarse_device(torch.from_numpy(xqt).cuda())
+    np.testing.assert_array_equal(Iq.cpu().numpy(), Iq2.cpu().numpy())
+    lists = Iq.cpu().numpy()
+    Dp, Ip = ix.search_preassigned(xq, k, lists)
+    Dpr, Ipr = ivf.search_preassigned(xqt, k, lists)
+    np.testing.assert_array_equal(Ip, Ipr)
+    Dc, Ic = np.zeros((16, k), np.float32), np.zeros((16, k), np.int64)
+    ix.search_preassigned(16, xq, k, lists, None, Dc, Ic, False)
+    np.testing.assert_array_equal(Ic, Ipr)
+    svc = RetrievalService(ix, batch_size=16, default_k=k, nprobe=4)
+    ans = svc.handle(wire.encode_request(xq, k, 16, d))
+    Ia, Da = wire.decode_answer(bytes(ans), k, 16)
+    np.testing.assert_array_equal(Ia, Iref)
+    np.testing.assert_array_equal(Da, Dref)
+    svl = RetrievalService(ix, batch_size=16, default_k=k, nprobe=4, request_with_lists=1)
+    ans = svl.handle(wire.encode_request_with_lists(xq, lists, 16, d, 4, k))
+    Ia, Da = wire.decode_answer(bytes(ans), k, 16)
+    np.testing.assert_array_equal(Ia, Ipr)
+    # apply on a side stream (the output allocated on that stream, ordered after the current one)
+    side = torch.cuda.Stream()
+    xd = torch.from_numpy(xq).cuda()
+    y = ix.chain.at(0).apply_device(xd, side.cuda_stream)
+    side.synchronize()
+    np.testing.assert_array_equal(y.cpu().numpy(), xqt)

@@ -199,3 +199,19 @@ def test_oracle_inner_product_semantics():
     D2, I2 = ox.search_preassigned(xq, k, lst, np.zeros_like(dis))
     np.testing.assert_array_equal(I2, I)
     np.testing.assert_array_equal(D2, D)
+
+
+def test_ip_kmeans_is_spherical_and_balanced():
+    """Inner-product k-means is spherical, as Faiss's IndexIVF sets it for
+    METRIC_INNER_PRODUCT (fvec_renorm_L2 after the initialization and after every
+    update): unit-norm centroids, and on raw non-negative data no few large-norm
+    centroids take almost every vector."""
+    rng = np.random.default_rng(3)
+    centres = rng.uniform(0, 128, (40, 32))
+    x = np.clip(np.rint(centres[rng.integers(0, 40, 8000)] + rng.normal(0, 16, (8000, 32))), 0, 255).astype(np.float32)
+    cent = O.kmeans(x, 32, 10, 5, nthreads=4, metric=O.METRIC_INNER_PRODUCT)
+    np.testing.assert_allclose(np.linalg.norm(cent.astype(np.float64), axis=1), 1.0, rtol=1e-5)
+    assign = np.argmax(x @ cent.T, axis=1)
+    sizes = np.bincount(assign, minlength=32)
+    assert sizes.max() < 0.25 * len(x), sizes
+    assert (sizes > 0).sum() >= 24, sizes
