@@ -99,7 +99,7 @@ def test_opq_index_full_surface():
     xt = datasets.synthetic_sift_like(4000, d, seed=21, n_centres=100)
     xb = datasets.synthetic_sift_like(8000, d, seed=22, n_centres=100)
     xq = datasets.synthetic_sift_like(16, d, seed=23, n_centres=100)
-    ix = faiss.index_factory(d, "OPQ4,IVF32,PQ4")
+    ix = faiss.index_factory(d, "OPQ8,IVF32,PQ8")
     ix.chain[0].niter = 2
     ix.train(xt)
     ix.add(xb)
