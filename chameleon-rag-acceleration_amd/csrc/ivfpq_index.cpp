@@ -177,7 +177,7 @@ struct ivfpq_index {
   DevBuf h_D, h_I, h_Iq, h_Dq;  // device staging of the host-buffer entry points
   DevBuf w_cand;                // segment candidates of the large-nlist coarse quantizer
   // list-major plan workspaces (ivfpq_kernels.h ListPlan)
-  DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_tau, p_qmask;
+  DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
   // Stream ordering of the per-handle workspaces: every device search records
   // `done` on its stream; the next search (on any stream) waits for it, and
   // anything that frees or rewrites device buffers synchronizes on it first.
@@ -213,9 +213,17 @@ struct ivfpq_index {
     }
     p_bucket.ensure(sizeof(int2) * 2 * (size_t)nloc * nq);
     p_recs.ensure(sizeof(int32_t) * 16 * (size_t)pl.max_items);
-    p_hdr.ensure(sizeof(int32_t) * 16);
+    if (!p_hdr.p) {  // hdr[2] (the scan's work counter) is kept zero between batches by k_merge_probes
+      p_hdr.ensure(sizeof(int32_t) * 16);
+      HIPCHECK(hipMemsetAsync(p_hdr.p, 0, p_hdr.bytes, s));
+    }
     p_D.ensure(sizeof(float) * nq * np * 4 * k);
     p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
+    p_N.ensure(sizeof(int32_t) * nq * np * 4);
+    if (!p_done.p || p_done.bytes < sizeof(int32_t) * nq) {  // kept zero between batches by k_merge_probes
+      p_done.ensure(sizeof(int32_t) * nq);
+      HIPCHECK(hipMemsetAsync(p_done.p, 0, p_done.bytes, s));
+    }
     p_tau.ensure(sizeof(int32_t) * nq);
     p_qmask.ensure(sizeof(uint64_t) * nq);
     pl.cnt = p_cnt.as<int32_t>();
@@ -224,9 +232,12 @@ struct ivfpq_index {
     pl.hdr = p_hdr.as<int32_t>();
     pl.partD = p_D.as<float>();
     pl.partI = p_I.as<int64_t>();
+    pl.partN = p_N.as<int32_t>();
+    pl.qdone = p_done.as<int32_t>();
     pl.tauq = p_tau.as<int32_t>();
     pl.qmask = p_qmask.as<uint64_t>();
     pl.order = d_order.p ? d_order.as<int32_t>() : nullptr;
+    pl.fused = scan_fused_plan(nloc, pl.max_items, M) ? 1 : 0;
     return pl;
   }
 

@@ -88,11 +88,14 @@ struct ListPlan {
   int32_t* hdr;      // [16]: n_items, n_items of kind 0, the list scan's work counter, 0...
   int max_items;
   float* partD;      // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k (keys)
-  int64_t* partI;    // same shape: global code positions (-1 = none)
+  int64_t* partI;    // same shape: global code positions (-1 = none; k <= 64 pads every list to k)
+  int32_t* partN;    // [nq][nprobe][4] valid entries of each partial list (k > 64 writes only those)
+  int32_t* qdone;    // [nq] k > 64: 1 = merged by k_merge_big (k_merge_probes resets it to 0)
   int32_t* tauq;     // [nq] running k-th key per query (order-preserving int of the float, atomicMin)
   uint64_t* qmask;   // [nq] probes the scan covers (nprobe <= 64): bit p = pair (q, p) is scanned
   int grid;          // persistent list-scan workgroups (multiple of 8)
   const int32_t* order = nullptr;  // [nloc] item order of the lists within a kind (nullable = list order)
+  int fused = 0;     // 1: the list scan derives its items from cnt/bucket (no k_plan_items launch, recs unused)
 };
 
 struct ScanArgs {
@@ -122,8 +125,10 @@ struct ScanArgs {
 void launch_plan_count(const int64_t* lists, const float* Dq, const float* x, const float* cent, int64_t nq, int d,
                        int nprobe, const int64_t* list_off, int lo, int hi, bool ip, bool dedup, int k,
                        const ListPlan& pl, hipStream_t s);
-// item records from the per-list counts (G = list_scan_group(M, k))
+// item records from the per-list counts (G = list_scan_group(M, k)); nothing to do when pl.fused
 void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int hi, int G, hipStream_t s);
+// whether the list scan can plan its own items (nloc lists, at most max_items items, code size M)
+bool scan_fused_plan(int nloc, int max_items, int M);
 
 int list_scan_group(int M, int k);  // pairs per work item (G) used for (M, k)
 int list_scan_max_items(int64_t npairs, int nloc, int G);

@@ -1123,6 +1123,7 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
           pl.partD[o + e] = FLT_MAX;
           pl.partI[o + e] = -1;
         }
+        for (int w = 0; w < 4; w++) pl.partN[(q * nprobe + p) * 4 + w] = 0;
       }
     }
     const uint64_t um = __ballot(use);
@@ -1425,6 +1426,10 @@ __device__ __forceinline__ void kc_bulk_merge_rows(PackedTopK<R>& tk, uint64_t c
     if (r + 1 < R) {
       c = hi;
       kc_steps<128, 32>(c, lane);
+      // c is ascending: when its smallest word is empty, so is every carry and
+      // the later rows keep their contents (a k = 1000 list holding a few hundred
+      // entries merges into its first rows only)
+      if (readlane_u64(c, 0) == kKcNone) break;
     }
   }
   tk.refresh_tau();
@@ -1542,6 +1547,126 @@ constexpr int QCAP = 256;  // per-wave candidate queue entries
   } while (0)
 #endif
 
+// ---- fused planning: the list scan derives its work items itself
+// (pl.fused: nloc <= kFusedPlanLists and fewer than 65536 items).  Every
+// workgroup forms the exclusive prefix of the per-list item counts
+// ceil(min(cnt, cap) / G) of both kinds in scheduling order (pl.order) in LDS;
+// item e of kind 0 ([0, N0)) or kind 1 ([N0, N)) is then found by a two-step
+// search over that prefix, and its record words are loaded from the counts,
+// list offsets and bucket in one round trip.  Replaces k_plan_items (one
+// launch) for the shard sizes where it fits in LDS.
+constexpr int kFusedPlanLists = 1024;
+
+// returns (N0, N1); ws: >= 8 ints of scratch (LDS)
+__device__ __forceinline__ int2 fused_plan_prefix(const ListPlan& pl, int nloc, int G, uint16_t* ex0, uint16_t* ex1,
+                                                  uint16_t* ord, int* ws) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // thread t: ranks 4t .. 4t + 3 (nloc <= 1024)
+  int a[4], b[4], sa = 0, sb = 0;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int j = 4 * tid + u;
+    const int jl = j < nloc ? (pl.order ? pl.order[j] : j) : 0;
+    a[u] = j < nloc ? (min(pl.cnt[jl], pl.cap) + G - 1) / G : 0;
+    b[u] = j < nloc ? (min(pl.cnt[nloc + jl], pl.cap) + G - 1) / G : 0;
+    if (j < nloc) ord[j] = (uint16_t)jl;
+    sa += a[u];
+    sb += b[u];
+  }
+  const int ia = wave_incl_scan(sa, lane), ib = wave_incl_scan(sb, lane);
+  if (lane == 63) {
+    ws[wave] = ia;
+    ws[4 + wave] = ib;
+  }
+  __syncthreads();
+  int pa = 0, pb = 0, ta = 0, tb = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    if (w < wave) {
+      pa += ws[w];
+      pb += ws[4 + w];
+    }
+    ta += ws[w];
+    tb += ws[4 + w];
+  }
+  pa += ia - sa;
+  pb += ib - sb;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int j = 4 * tid + u;
+    if (j < nloc) {
+      ex0[j] = (uint16_t)pa;
+      ex1[j] = (uint16_t)pb;
+    }
+    pa += a[u];
+    pb += b[u];
+  }
+  if (tid == 0) {
+    ex0[nloc] = (uint16_t)ta;
+    ex1[nloc] = (uint16_t)tb;
+  }
+  __syncthreads();
+  return make_int2(ta, tb);
+}
+
+// word (lane & 15) of item e's record (layout of write_item)
+__device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& pl, int nloc, int G, int e, int n0,
+                                            const uint16_t* ex0, const uint16_t* ex1, const uint16_t* ord, int lane) {
+  const int kind = e < n0 ? 0 : 1;
+  const int ek = kind ? e - n0 : e;
+  const uint16_t* ex = kind ? ex1 : ex0;
+  // largest j with ex[j] <= ek: first over every 16th rank, then within 16 ranks
+  const int c16 = (nloc + 15) >> 4;
+  const uint64_t m1 = __builtin_amdgcn_ballot_w64(lane < c16 && (int)ex[16 * lane] <= ek);
+  const int j0 = 16 * (63 - __builtin_clzll(m1));
+  const uint64_t m2 = __builtin_amdgcn_ballot_w64(lane < 16 && j0 + lane < nloc && (int)ex[j0 + lane] <= ek);
+  const int j = j0 + 63 - __builtin_clzll(m2);
+  const int jl = ord[j];
+  const int t = ek - (int)ex[j];
+  const int64_t l = a.list_lo + jl;
+  const int w = lane & 15;
+  int v = 0;
+  if (w == 0) {
+    v = (int)l;
+  } else if (w == 1) {
+    v = min(G, min(pl.cnt[kind * nloc + jl], pl.cap) - t * G);
+  } else if (w == 2) {
+    v = (int)(a.list_off[l + 1] - a.list_off[l]);
+  } else if (w <= 4) {
+    const int64_t b = a.list_off[l];
+    v = w == 3 ? (int)(uint32_t)(uint64_t)b : (int)(uint32_t)((uint64_t)b >> 32);
+  } else if (w <= 12) {  // slots past the item's count hold other pairs: never used
+    const int g = (w - 5) & 3;
+    const int2 be = pl.bucket[((int64_t)jl * 2 + kind) * pl.cap + min(t * G + g, pl.cap - 1)];
+    v = w <= 8 ? be.x : be.y;
+  } else if (w == 13) {
+    v = kind;
+  }
+  return v;
+}
+
+// A wave's sorted partial list of one pair into slot `slot` = pair * 4 + wave:
+// k <= 64 pads the list to k entries ((FLT_MAX, -1)); k > 64 writes the valid
+// entries and their count only (k_merge_big reads partN).
+template <int R>
+__device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTopK<R>& tk, int64_t slot, int k,
+                                              int64_t beg, int lane) {
+  const int64_t o = slot * k;
+  int n = 0;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int ix = r * 64 + lane;
+    const bool empty = tk.p[r] == kKcNone;
+    if (ix < k && (R == 1 || !empty)) {
+      pl.partD[o + ix] = empty ? FLT_MAX : kc_key(tk.p[r]);
+      pl.partI[o + ix] = empty ? -1 : beg + (int64_t)(uint32_t)tk.p[r];  // global code position
+    }
+    if constexpr (R >= 2) n += __popcll(__builtin_amdgcn_ballot_w64(ix < k && !empty));
+  }
+  if constexpr (R >= 2)
+    if (lane == 0) pl.partN[slot] = n;
+}
+
 template <int M, int G, int R, int JB>
 __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) {
   using V = typename LutVec<G>::T;
@@ -1553,6 +1678,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   __shared__ int32_t qi[4][QCAP];  // positions in the list
   __shared__ int s_next;
   __shared__ int32_t s_wb[G];  // the item's per-query bounds found by its waves (ordered ints)
+  // fused planning (pl.fused): the item prefix of every list in scheduling order
+  __shared__ uint16_t s_ex[2][kFusedPlanLists + 1];
+  __shared__ uint16_t s_ord[kFusedPlanLists];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1560,16 +1688,23 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   const int k = a.k;
   const int ip = a.ip;
   const int nloc = a.list_hi - a.list_lo;
-  if (blockIdx.x == 0)  // the counts were consumed by k_plan_items: zero them for the next batch
-    for (int i = tid; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
-  const int n_items = pl.hdr[0];
   const uint64_t lanemask_lt = (1ull << lane) - 1;
+  int n_items, n_items0 = 0;
+  if (pl.fused) {
+    const int2 t = fused_plan_prefix(pl, nloc, G, s_ex[0], s_ex[1], s_ord, reinterpret_cast<int*>(qi));
+    n_items0 = t.x;
+    n_items = t.x + t.y;
+  } else {
+    n_items = pl.hdr[0];
+  }
 
   // An item's 64-B record: lanes 0..15 load its 16 words (vector loads, kept in
-  // flight while the previous item is scanned), unpacked with readlane.
+  // flight while the previous item is scanned), unpacked with readlane.  Fused
+  // planning derives the words from the LDS prefix, the counts and the buckets.
   Item<G> it;
   auto fetch_rec = [&](int idx) __attribute__((always_inline)) -> int {
-    return pl.recs[(int64_t)idx * 16 + (lane & 15)];
+    if (!pl.fused) return pl.recs[(int64_t)idx * 16 + (lane & 15)];
+    return fused_record(a, pl, nloc, G, idx, n_items0, s_ex[0], s_ex[1], s_ord, lane);
   };
   auto unpack = [&](int rv) __attribute__((always_inline)) {
     it.l = __builtin_amdgcn_readlane(rv, 0);
@@ -1964,16 +2099,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
     for (int g = 0; g < G; g++) {
       if (g >= ci.cnt) continue;
-      const int64_t o = ((int64_t)ci.pair[g] * 4 + wave) * k;
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        const int ix = r * 64 + lane;
-        if (ix < k) {
-          const bool empty = tk[g].p[r] == kKcNone;
-          pl.partD[o + ix] = empty ? FLT_MAX : kc_key(tk[g].p[r]);
-          pl.partI[o + ix] = empty ? -1 : ci.beg + (int64_t)(uint32_t)tk[g].p[r];  // global code position
-        }
-      }
+      write_partial<R>(pl, tk[g], (int64_t)ci.pair[g] * 4 + wave, k, ci.beg, lane);
     }
     DIAG(3, __builtin_amdgcn_s_memtime());
     it_no++;
@@ -2201,16 +2327,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_skew16(ScanArgs a, ListPlan pl)
 #pragma unroll
     for (int g = 0; g < G; g++) {
       if (g >= wcnt) continue;
-      const int64_t o = ((int64_t)w.pair(g) * 4 + wave) * k;
-#pragma unroll
-      for (int r = 0; r < R; r++) {
-        const int ix = r * 64 + lane;
-        if (ix < k) {
-          const bool empty = tk[g].p[r] == kKcNone;
-          pl.partD[o + ix] = empty ? FLT_MAX : kc_key(tk[g].p[r]);
-          pl.partI[o + ix] = empty ? -1 : wbeg + (int64_t)(uint32_t)tk[g].p[r];  // global code position
-        }
-      }
+      write_partial<R>(pl, tk[g], (int64_t)w.pair(g) * 4 + wave, k, wbeg, lane);
       if (wave == 0 && lane == 0) {
         const int32_t wb = s_wb[g];
         if (wb != f2ord(kInf)) atomicMin(&pl.tauq[qof(w, g)], wb);
@@ -2593,7 +2710,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_skew16(ScanArgs a, ListPlan pl)
     pit = it;
     have_pit = true;
     SKEW_STAMP(5, __builtin_amdgcn_s_memtime());
-    SKEW_STAMP(6, (uint32_t)it.n | ((uint64_t)it.kind << 32) | ((uint64_t)it.cnt << 40) | ((uint64_t)nblk << 48));
+    SKEW_STAMP(6, (uint32_t)it.n() | ((uint64_t)__builtin_amdgcn_readlane(it.rv, 13) << 32) | ((uint64_t)it.cnt() << 40) | ((uint64_t)nblk << 48));
     it_no++;
     it = nit;
     cur = nxt;
@@ -2715,6 +2832,11 @@ template <int R>
 __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   constexpr int B = 4;
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0) {  // the scan consumed the counts and its work counter: zero them for the next batch
+    const int nloc = a.list_hi - a.list_lo;
+    for (int i = threadIdx.x; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
+    if (threadIdx.x == 0) pl.hdr[2] = 0;
+  }
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= a.nq) return;
   const int k = a.k;
@@ -2778,183 +2900,13 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     }
   }
   if constexpr (R >= 2) {
-    // k > 64, nprobe <= 64: bound first, then merge only the entries under the bound.
-    // S = the first s entries of each of the L = 4 nprobe sorted partial lists
-    // (L s >= k); S is a subset of all entries, so its k-th smallest key T bounds
-    // the final k-th key -- and equals it whenever no list contributes more than
-    // s entries to the top-k, so s is as large as SV slots per lane allow.  T is
-    // found by a bisection on the order-preserving integer of the keys (32
-    // ballot-count rounds).  Then every list's prefix <= T is compacted into LDS
-    // and only those candidates get their labels looked up and enter the
-    // (key, label) top-k.  Too many candidates (ties) fall through to the full
-    // merge below.
-    constexpr int CAP = R <= 8 ? 1024 : 128 * R;  // candidates per wave (>= 2k)
-    constexpr int CAP2 = R <= 8 ? CAP : 0;         // second bisection over up to CAP2 candidates
-    constexpr int SV = R + 4 > 16 ? R + 4 : 16;  // S slots per lane (64 SV >= k + 256 > k + L - 1)
-    __shared__ float cd_s[4][CAP];
-    __shared__ int64_t cp_s[4][CAP];
+    // k > 64, nprobe <= 64: k_merge_big ran first and merged every query whose
+    // candidates fit its buffer; the rest (ties) take the full merge below
     if (np <= 64) {
-      const int wave = threadIdx.x >> 6;
-      const int L = 4 * np;
-      const int s = min(k, 64 * SV / L);  // L s >= 64 SV - L + 1 > k
-      const int NS = L * s;
-      const uint64_t qm = pl.qmask[q];
-      auto ukey = [](float v) __attribute__((always_inline)) {
-        return (uint32_t)f2ord(v + 0.0f) ^ 0x80000000u;  // unsigned order == float order (-0 folded)
-      };
-      uint32_t u[SV];
-      int nvalid = 0;
-#pragma unroll
-      for (int t = 0; t < SV; t++) {
-        const int e = t * 64 + lane;
-        const int j = e % L, i = e / L;
-        const bool in = e < NS && ((qm >> (j >> 2)) & 1);
-        const int64_t at = ((q * np + (j >> 2)) * 4 + (j & 3)) * (int64_t)k + (in ? i : 0);
-        const int64_t pos = in ? pl.partI[at] : -1;
-        const float dv = in ? pl.partD[at] : kInf;
-        const bool ok = pos >= 0;
-        u[t] = ok ? ukey(dv) : 0xFFFFFFFFu;
-        nvalid += __popcll(__builtin_amdgcn_ballot_w64(ok));
-      }
-      uint32_t Tu = 0xFFFFFFFEu;  // fewer than k entries in S: every valid entry is a candidate
-      if (nvalid >= k) {
-        uint32_t lo = 0, hi = 0xFFFFFFFEu;
-        while (lo < hi) {
-          const uint32_t mid = lo + ((hi - lo) >> 1);
-          int cnt = 0;
-#pragma unroll
-          for (int t = 0; t < SV; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u[t] <= mid));
-          if (cnt >= k) hi = mid; else lo = mid + 1;
-        }
-        Tu = lo;
-      }
-      // per list: the length of its prefix <= T (lists sorted, valid entries first)
-      int c[4] = {0, 0, 0, 0};
-      int mine = 0;
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const int j = t * 64 + lane;
-        if (j < L && ((qm >> (j >> 2)) & 1)) {
-          const int64_t base = ((q * np + (j >> 2)) * 4 + (j & 3)) * (int64_t)k;
-          int n = 0;
-          bool go = true;
-          while (go && n < k) {
-            float dv[8];
-            int64_t pv[8];
-#pragma unroll
-            for (int h = 0; h < 8; h++) {
-              const int i = min(n + h, k - 1);
-              dv[h] = pl.partD[base + i];
-              pv[h] = pl.partI[base + i];
-            }
-#pragma unroll
-            for (int h = 0; h < 8; h++) {
-              if (go && n < k && pv[h] >= 0 && ukey(dv[h]) <= Tu) n++;
-              else go = false;
-            }
-          }
-          c[t] = n;
-          mine += n;
-        }
-      }
-      const int incl = wave_incl_scan(mine, lane);
-      int C = __builtin_amdgcn_readlane(incl, 63);
-      if (C <= CAP) {
-        int o = incl - mine;
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int j = t * 64 + lane;
-          if (c[t] > 0) {
-            const int64_t base = ((q * np + (j >> 2)) * 4 + (j & 3)) * (int64_t)k;
-            for (int i = 0; i < c[t]; i++, o++) {
-              cd_s[wave][o] = pl.partD[base + i];
-              cp_s[wave][o] = pl.partI[base + i];
-            }
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if constexpr (CAP2 > 0) {
-          // A list holding more than s of the top-k leaves T loose: tighten it by a
-          // second bisection over the compacted candidates (held in registers),
-          // then keep only those <= T2 at the front of the buffer (in place: an
-          // entry only moves to a lower index, and every slot is read by the whole
-          // wave before it is written).
-          if (C > 2 * k) {
-            uint32_t u2[CAP2 / 64];
-#pragma unroll
-            for (int t = 0; t < CAP2 / 64; t++) {
-              const int e = t * 64 + lane;
-              u2[t] = e < C ? ukey(cd_s[wave][e]) : 0xFFFFFFFFu;
-            }
-            uint32_t lo = 0, hi = 0xFFFFFFFEu;
-            while (lo < hi) {
-              const uint32_t mid = lo + ((hi - lo) >> 1);
-              int cnt = 0;
-#pragma unroll
-              for (int t = 0; t < CAP2 / 64; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u2[t] <= mid));
-              if (cnt >= k) hi = mid; else lo = mid + 1;
-            }
-            int n2 = 0;
-#pragma unroll
-            for (int t = 0; t < CAP2 / 64; t++) {
-              const int e = t * 64 + lane;
-              const bool keep = e < C && u2[t] <= lo;
-              const uint64_t mk = __builtin_amdgcn_ballot_w64(keep);
-              if (mk) {
-                const float dv = cd_s[wave][e < C ? e : 0];
-                const int64_t pv = cp_s[wave][e < C ? e : 0];
-                __builtin_amdgcn_wave_barrier();
-                if (keep) {
-                  const int at = n2 + __popcll(mk & ((1ull << lane) - 1));
-                  cd_s[wave][at] = dv;
-                  cp_s[wave][at] = pv;
-                }
-                n2 += __popcll(mk);
-              }
-            }
-            C = n2;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          }
-        }
-        WaveTopK<R> tb;
-        tb.init(k);
-        for (int g0 = 0; g0 < C; g0 += 64 * 4) {
-          // labels of up to 4 batches in flight at once
-          int64_t idb[4];
-          float db[4];
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            const int e = g0 + b * 64 + lane;
-            db[b] = e < C ? cd_s[wave][e] : kInf;
-            idb[b] = e < C ? a.ids[cp_s[wave][e]] : kSentinelId;
-          }
-#pragma unroll
-          for (int b = 0; b < 4; b++) {
-            const int e = g0 + b * 64 + lane;
-            const bool pass = e < C && lexless(db[b], idb[b], tb.td, tb.ti);
-            const uint64_t mask = __ballot(pass);
-            if (!mask) continue;
-            if (__popcll(mask) > 6)
-              bulk_merge_rows(tb, pass ? db[b] : kInf, pass ? idb[b] : kSentinelId, lane);
-            else
-              tb.insert(mask, db[b], idb[b], lane);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-          const int idx = r * 64 + lane;
-          if (idx < k) {
-            const bool empty = tb.id[r] == kSentinelId;
-            a.outD[q * k + idx] = empty ? pad : sgn * tb.d[r];
-            a.outI[q * k + idx] = empty ? -1 : tb.id[r];
-          }
-        }
-        return;
-      }
+      const int done = pl.qdone[q];
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) pl.qdone[q] = 0;  // zero for the next batch
+      if (done) return;
     }
   }
   // Full merge.  For k > 64 the entries are visited rank-major across the
@@ -2988,7 +2940,8 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
           const int64_t l = a.probe_list[q * np + p];
           scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
         }
-        if (scanned) {
+        // k > 64 writes only each list's valid prefix (partN entries)
+        if (scanned && (R == 1 || i < pl.partN[q * (int64_t)L + j])) {
           const int64_t at = qbase + (int64_t)j * k + i;
           d[b] = pl.partD[at];
           pos[b] = pl.partI[at];
@@ -3026,6 +2979,231 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       a.outI[q * k + idx] = empty ? -1 : tk.id[r];
     }
   }
+}
+
+// ------------------------------------------------- probe merge, k > 64
+// One wave per query (nprobe <= 64).  The L = 4 nprobe per-wave partial lists
+// of the query's scanned probes are sorted by (key, position) and hold
+// partN[j] valid entries each (k > 64: only those are written).
+//  1. Candidate prefixes: every list entirely (C = sum of lengths).
+//  2. While C > CAP: sample each list's prefix at stride r = ceil(C / NS)
+//     (positions r-1, 2r-1, ...); if the lists hold m_j samples <= v, at least
+//     r * sum m_j entries are <= v, so the ceil(k / r)-th smallest sample T
+//     bounds the final k-th key.  Each list's prefix <= T is found by binary
+//     search; C shrinks to at most k + r + L r per round (r = 1: exact).
+//  3. The prefixes are compacted into LDS; the exact k-th key (bisection on
+//     the order-preserving integers) cuts them to the k best and their ties.
+//  4. Labels for those only; one bitonic sort by (key, label) in LDS.
+// Queries whose ties overflow CAP are left to k_merge_probes' full merge
+// (flag in pl.qdone).  Replaces the per-query selection of faiss-gpu's
+// pass2SelectLists (classify_stages.py:127-136; 78 % of the time at K = 1000,
+// MICRO_GPU_profiling/out_img/profile_experiment_5_topK.png).
+constexpr int kBigCap = 2048;
+
+__device__ __forceinline__ uint32_t ukey_of(float v) {
+  return (uint32_t)f2ord(v + 0.0f) ^ 0x80000000u;  // unsigned order == float order (-0 folded)
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// the kk-th smallest (1-based) of the wave's NV x 64 values (0xFFFFFFFF = absent);
+// requires kk <= the number of present values
+template <int NV>
+__device__ __forceinline__ uint32_t wave_kth_u32(const uint32_t (&u)[NV], int kk) {
+  uint32_t lo = 0, hi = 0xFFFFFFFEu;
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int cnt = 0;
+#pragma unroll
+    for (int t = 0; t < NV; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u[t] <= mid));
+    if (cnt >= kk) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
+  constexpr int SV = 20;  // sample slots per lane
+  __shared__ float cd[kBigCap];
+  __shared__ int64_t cl[kBigCap];  // code positions, then labels
+  __shared__ int lens[257];        // per-list candidate prefix lengths, then exclusive offsets
+  __shared__ int sp[257];          // exclusive prefix of the per-list sample counts
+  const int lane = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  const int k = a.k, np = a.nprobe, L = 4 * np;
+  const uint64_t qm = pl.qmask[q];
+  const int64_t qb = q * (int64_t)L;  // list j: entries at (qb + j) * k + i
+  const float pad = a.ip ? -FLT_MAX : FLT_MAX;
+  const float sgn = a.ip ? -1.f : 1.f;
+  auto key_at = [&](int j, int i) __attribute__((always_inline)) { return pl.partD[(qb + j) * k + i]; };
+
+  int C = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int j = t * 64 + lane;
+    const int n = (j < L && ((qm >> (j >> 2)) & 1)) ? min(pl.partN[qb + j], k) : 0;
+    lens[j] = n;
+    C += n;
+  }
+  C = wave_sum_i(C);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t Tu = 0xFFFFFFFFu;  // every entry is a candidate
+  for (int round = 0; C > kBigCap && round < 8; round++) {
+    const int r = (C + 64 * SV - 1) / (64 * SV);
+    // exclusive prefix of per-list sample counts (lists in j order: 4 scans of 64)
+    int carry = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int j = t * 64 + lane;
+      const int c = lens[j] / r;
+      const int incl = wave_incl_scan(c, lane);
+      sp[j] = carry + incl - c;
+      carry += __builtin_amdgcn_readlane(incl, 63);
+    }
+    if (lane == 0) sp[256] = carry;
+    __builtin_amdgcn_wave_barrier();
+    const int S = carry, K2 = (k + r - 1) / r;
+    if (S < K2) break;  // too few samples to bound (cannot happen for C > kBigCap, L <= 256)
+    uint32_t u[SV];
+#pragma unroll
+    for (int t = 0; t < SV; t++) {
+      const int e = t * 64 + lane;
+      u[t] = 0xFFFFFFFFu;
+      if (e < S) {
+        int lo = 0, hi = 256;  // largest j with sp[j] <= e
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (sp[mid] <= e) lo = mid; else hi = mid;
+        }
+        u[t] = ukey_of(key_at(lo, (e - sp[lo] + 1) * r - 1));
+      }
+    }
+    Tu = wave_kth_u32<SV>(u, K2);
+    // each list's prefix <= Tu, by binary search over its current prefix
+    C = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int j = t * 64 + lane;
+      int lo = 0, hi = lens[j];
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ukey_of(key_at(j, mid)) <= Tu) lo = mid + 1; else hi = mid;
+      }
+      lens[j] = lo;
+      C += lo;
+    }
+    C = wave_sum_i(C);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (C > kBigCap) return;  // ties overflow: the full merge of k_merge_probes takes this query
+  // compact the prefixes (offsets in j order)
+  {
+    int carry = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int j = t * 64 + lane;
+      const int c = lens[j];
+      const int incl = wave_incl_scan(c, lane);
+      sp[j] = carry + incl - c;
+      carry += __builtin_amdgcn_readlane(incl, 63);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // lane-parallel over the flat candidate index: one coalesced pass per 64
+    for (int e0 = 0; e0 < C; e0 += 64) {
+      const int e = e0 + lane;
+      if (e < C) {
+        int lo = 0, hi = 256;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (sp[mid] <= e) lo = mid; else hi = mid;
+        }
+        const int64_t at = (qb + lo) * k + (e - sp[lo]);
+        cd[e] = pl.partD[at];
+        cl[e] = pl.partI[at];
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the exact k-th key: keep the k best and their ties (in place, order kept)
+  if (C > k) {
+    uint32_t u2[kBigCap / 64];
+#pragma unroll
+    for (int t = 0; t < kBigCap / 64; t++) {
+      const int e = t * 64 + lane;
+      u2[t] = e < C ? ukey_of(cd[e]) : 0xFFFFFFFFu;
+    }
+    const uint32_t T2 = wave_kth_u32<kBigCap / 64>(u2, k);
+    int n2 = 0;
+#pragma unroll
+    for (int t = 0; t < kBigCap / 64; t++) {
+      const int e = t * 64 + lane;
+      const bool keep = e < C && u2[t] <= T2;
+      const uint64_t mk = __builtin_amdgcn_ballot_w64(keep);
+      if (mk) {  // wave-uniform
+        const float dv = cd[e < C ? e : 0];
+        const int64_t pv = cl[e < C ? e : 0];
+        __builtin_amdgcn_wave_barrier();
+        if (keep) {
+          const int at = n2 + __popcll(mk & ((1ull << lane) - 1));
+          cd[at] = dv;
+          cl[at] = pv;
+        }
+        n2 += __popcll(mk);
+      }
+    }
+    C = n2;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // labels, and padding up to the sort size P (a power of two)
+  int P = 64;
+  while (P < C) P <<= 1;
+  for (int e = lane; e < P; e += 64) {
+    if (e < C) {
+      cl[e] = a.ids[cl[e]];
+    } else {
+      cd[e] = kInf;
+      cl[e] = kSentinelId;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // bitonic sort of P entries by (key, label), ascending
+  for (int sz = 2; sz <= P; sz <<= 1) {
+    for (int st = sz >> 1; st > 0; st >>= 1) {
+      for (int p0 = 0; p0 < P / 2; p0 += 64) {
+        const int pi = p0 + lane;  // compare pair index
+        const int i = ((pi / st) * 2 * st) + (pi % st);
+        const int j = i + st;
+        const bool up = (i & sz) == 0;
+        const float di = cd[i], dj = cd[j];
+        const int64_t li = cl[i], lj = cl[j];
+        const bool sw = lexless(dj, lj, di, li) == up;  // pairs of a stage are disjoint
+        if (sw) {
+          cd[i] = dj;
+          cl[i] = lj;
+          cd[j] = di;
+          cl[j] = li;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  for (int e = lane; e < k; e += 64) {
+    const bool empty = e >= C;
+    a.outD[q * k + e] = empty ? pad : sgn * cd[e];
+    a.outI[q * k + e] = empty ? -1 : cl[e];
+  }
+  if (lane == 0) pl.qdone[q] = 1;
 }
 
 // ------------------------------------------------------------ shard merge
@@ -3229,7 +3407,12 @@ void launch_plan_count(const int64_t* lists, const float* Dq, const float* x, co
                      list_off, lo, hi, ip ? 1 : 0, dedup ? 1 : 0, k, pl);
 }
 
+bool scan_fused_plan(int nloc, int max_items, int M) {
+  return nloc <= kFusedPlanLists && max_items < 65536 && !codes_rotated(M);
+}
+
 void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int hi, int G, hipStream_t s) {
+  if (pl.fused) return;  // the list scan plans its own items
   const int nloc = hi - lo;
   if (nloc <= kPlanSmall)
     hipLaunchKernelGGL(k_plan_items_small, dim3(std::max(1u, nblocks(pl.max_items, PLAN_T))), dim3(PLAN_T), 0, s, pl,
@@ -3240,7 +3423,10 @@ void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int 
 }
 
 bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 || M == 64; }
-bool codes_rotated(int M) { return M == 16; }
+#ifndef SCAN_SKEW16
+#define SCAN_SKEW16 0  // 1: M = 16 by k_scan_skew16 over rotated codes (r03 A/B: 144 vs 120 us, kept off)
+#endif
+bool codes_rotated(int M) { return SCAN_SKEW16 && M == 16; }
 
 #ifndef SCAN_G_MAX
 #define SCAN_G_MAX 4  // pairs per work item (A/B builds may lower it)
@@ -3281,7 +3467,7 @@ int scan_lists_grid(int M, int k) {
   const int per_cu = SCAN_WG_PER_CU;
 #else
   // workgroups per CU the LDS allows (LUTs + candidate queues), at most 3
-  const int lds = M * 256 * 4 * list_scan_group(M, k) + 4 * QCAP * 8 + 64;
+  const int lds = M * 256 * 4 * list_scan_group(M, k) + 4 * QCAP * 8 + 6 * kFusedPlanLists + 96;
   const int per_cu = std::max(1, std::min(3, 160 * 1024 / lds));
 #endif
   return std::max(8, (per_cu * cus + 7) / 8 * 8);
@@ -3295,7 +3481,7 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
 #endif
   constexpr int JB = M <= 16 ? SCAN_JB16 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs), even
   if (ev) (void)hipEventRecord(ev[0], s);
-  if constexpr (M == 16)  // rotated device codes (codes_rotated(16)): the conflict-free scan
+  if constexpr (M == 16 && SCAN_SKEW16)  // rotated device codes (codes_rotated(16)): the conflict-free scan
     hipLaunchKernelGGL((k_scan_skew16<G, R>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   else
     hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
@@ -3304,6 +3490,7 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
 #endif
   if (ev) (void)hipEventRecord(ev[1], s);
+  if (R >= 2 && a.nprobe <= 64) hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
 

@@ -127,6 +127,32 @@ def synthetic_sift_like(n, d=128, seed=1234, n_centres=10000, sigma=16.0, centre
     return out
 
 
+def embed_like(x, mu):
+    """Centred, unit-norm rows (sentence-embedding-like, the C3 shape): the raw
+    non-negative synthetic rows have one dominant direction, which inner-product
+    search would rank by norm alone."""
+    y = x - mu
+    return np.ascontiguousarray(y / np.maximum(np.linalg.norm(y, axis=1, keepdims=True), 1e-6), np.float32)
+
+
+def c3_nq_shaped(nb=2_680_000, nt=200_000, nq=4096, d=768, n_centres=20000, seed0=7, chunk=500_000):
+    """The C3 (BEIR-NQ-shaped) synthetic set: 768-d embedding-like rows
+    (embed_like of synthetic_sift_like, centred on the training mean).
+    Returns (xt, base chunk generator, xq); the base set is yielded in chunks of
+    `chunk` rows (seeds 1000 + seed0 + i0), so 2.68 M x 768 floats never sit in
+    host memory at once."""
+    xt = synthetic_sift_like(nt, d, seed=4321 + seed0, n_centres=n_centres)
+    mu = xt.mean(0, keepdims=True)
+    xq = embed_like(synthetic_sift_like(nq, d, seed=123, n_centres=n_centres), mu)
+
+    def base():
+        for i0 in range(0, nb, chunk):
+            yield embed_like(synthetic_sift_like(min(chunk, nb - i0), d, seed=1000 + seed0 + i0,
+                                                 n_centres=n_centres), mu)
+
+    return embed_like(xt, mu), base, xq
+
+
 def sift1m_shaped(nb=1_000_000, nt=100_000, nq=10_240, d=128):
     """The C2 synthetic workload: base seed 1234, train 4321, queries 123."""
     xb = synthetic_sift_like(nb, d, seed=1234)

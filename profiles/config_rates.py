@@ -96,8 +96,14 @@ def main():
         del ix, xq
     if "c3" in only:
         t0 = time.time()
-        ix, mu = build(faiss, datasets, 768, 4096, 64, a.c3_nb, 200_000, 6, faiss.METRIC_INNER_PRODUCT, 20000, 7)
-        xq = torch.from_numpy(embed_like(datasets.synthetic_sift_like(4096, 768, seed=123, n_centres=20000), mu)).cuda()
+        # the index tests/test_gpu_fullsize.py checks against the oracle (datasets.c3_nq_shaped)
+        xt, base, xq = datasets.c3_nq_shaped(nb=a.c3_nb)
+        ix = faiss.index_factory(768, "IVF4096,PQ64", faiss.METRIC_INNER_PRODUCT, device=0)
+        ix.niter_coarse = ix.niter_pq = 6
+        ix.train(xt)
+        for xb in base():
+            ix.add(xb)
+        xq = torch.from_numpy(xq).cuda()
         ix.nprobe = 32
         for k in (10, 1000):
             r = rate(ix, xq, k, a.reps)

@@ -266,3 +266,49 @@ def test_segmented_coarse_matches_oracle(nq, nprobe):
     Dr, Ir = O.coarse_search(xq, cent, nprobe)
     np.testing.assert_array_equal(Iq.cpu().numpy(), Ir)
     np.testing.assert_array_equal(Dq.cpu().numpy(), Dr)
+
+
+@pytest.mark.parametrize("k", [10, 100])
+def test_c4_shape_eight_list_range_shards(c4_shape, k):
+    """C4's list-sharded form at its shape (d 96, M 48, nlist 65536, nprobe 32)
+    on one GPU: 8 list-range handles, each running the segmented coarse
+    quantizer on its own query slice, the probes concatenated (the all_gather),
+    each scanning its lists for the whole batch, and each slice's 8 partials
+    merged on the device (the all_to_all + merge).  Must equal the unsharded
+    oracle bit for bit (reference: IndexShards over 8 GPUs,
+    bench_gpu_1bn.py:605-616)."""
+    import torch
+
+    ix, ox, xq = c4_shape
+    N = 8
+    ox.nprobe = 32
+    sizes = ix.invlists.list_sizes()
+    ranges = balanced_list_ranges(sizes, N, ix.M)
+    xd = torch.from_numpy(xq).cuda()
+    B = xd.shape[0] // N
+    shards = []
+    for lo, hi in ranges:
+        sh = faiss.IndexIVFPQ(None, ix.d, ix.nlist, ix.M, 8, device=0)
+        sh.set_trained(ix.centroids(), ix.codebook())
+        sh.set_list_range(lo, hi)
+        lists = [l for l in range(lo, hi) if sizes[l]]
+        if lists:
+            sh.add_preencoded(np.concatenate([np.full(sizes[l], l, np.int64) for l in lists]),
+                              np.concatenate([ix.invlists.get_codes(l).reshape(-1, ix.M) for l in lists]),
+                              np.concatenate([ix.invlists.get_ids(l) for l in lists]))
+        sh.nprobe = 32
+        shards.append(sh)
+    probes = [shards[r].coarse_device(xd[r * B:(r + 1) * B]) for r in range(N)]
+    Dq = torch.cat([p[0] for p in probes])
+    Iq = torch.cat([p[1] for p in probes])
+    parts = [sh.search_preassigned_device(xd, k, Iq, Dq) for sh in shards]
+    Dm, Im = [], []
+    for r in range(N):
+        D, I = faiss.merge_topk_device(torch.stack([p[0][r * B:(r + 1) * B] for p in parts]),
+                                       torch.stack([p[1][r * B:(r + 1) * B] for p in parts]))
+        Dm.append(D)
+        Im.append(I)
+    torch.cuda.synchronize()
+    del shards, parts
+    Dr, Ir = ox.search(xq, k)
+    assert_same(torch.cat(Dm).cpu().numpy(), torch.cat(Im).cpu().numpy(), Dr, Ir)
