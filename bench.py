@@ -155,10 +155,13 @@ def main():
     bytes_lists = bytes_alg
 
     merged = {}
+    side = torch.cuda.Stream(dev) if shard else None
 
     def step(b):
         if shard:  # coarse for this rank's slice, probes all-gathered, own lists scanned for the batch
             xg = xq_dev[b]
+            # T3 of the global batch on a side stream, concurrent with the coarse step and the all_gather
+            ix.precompute_tables_device(xg, stream=side.cuda_stream)
             Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
             Dq, Iq = all_gather_probes(Dq_s, Iq_s, world)
             Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbuf, Ibuf)

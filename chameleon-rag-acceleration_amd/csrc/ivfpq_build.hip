@@ -1,0 +1,178 @@
+// Device-side inverted-list image build (ivfpq_add_device, and the host add
+// path routed through it): the new entries' (list, label, code) arrays are
+// merged with the current list-contiguous image into a new image, entirely on
+// the GPU.  Faiss appends to per-list vectors on the host
+// (InvertedLists::add_entries, Chameleon/Faiss_experiments/bench_gpu_1bn.py:
+// 598-658 adds 1e9 vectors in 1e6-vector slices); here a 1e9 / 8 shard
+// (125 M codes) is rebuilt in HBM without a host round trip.
+//
+// Order: stable by (list, label) -- two LSD radix sorts (label, then list),
+// rocprim's radix sort being stable -- which is the device image's within-list
+// label order.  Entries whose list lies outside the handle's
+// range [lo, hi) are dropped (a list-range shard keeps its own lists only).
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "ivfpq_build.h"
+
+namespace chivf {
+
+namespace {
+
+inline unsigned nblk(int64_t n, int t) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+// list number of every entry of the current image (from its offsets); one workgroup per list
+__global__ __launch_bounds__(256) void k_expand_lists(const int64_t* __restrict__ off, int lo, int hi,
+                                                      uint32_t* __restrict__ lno) {
+  const int l = lo + blockIdx.x;
+  if (l >= hi) return;
+  for (int64_t i = off[l] + threadIdx.x; i < off[l + 1]; i += 256) lno[i] = (uint32_t)l;
+}
+
+// new entries: list numbers (int64, from the coarse assignment) -> sort keys;
+// outside [lo, hi) -> nlist (sorted after every kept entry)
+__global__ __launch_bounds__(256) void k_new_keys(const int64_t* __restrict__ lists, int64_t n, int lo, int hi,
+                                                  int nlist, uint32_t* __restrict__ lno) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t l = lists[i];
+  lno[i] = (l >= lo && l < hi) ? (uint32_t)l : (uint32_t)nlist;
+}
+
+__global__ __launch_bounds__(256) void k_iota_u32(uint32_t* __restrict__ v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void k_iota_i64(int64_t* __restrict__ v, int64_t n, int64_t start) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) v[i] = start + i;
+}
+
+// the labels of all entries (old image then new), in source order
+__global__ __launch_bounds__(256) void k_concat_ids(const int64_t* __restrict__ a, int64_t na,
+                                                    const int64_t* __restrict__ b, int64_t nb,
+                                                    int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < na) out[i] = a[i];
+  else if (i < na + nb) out[i] = b[i - na];
+}
+
+__global__ __launch_bounds__(256) void k_gather_keys(const uint32_t* __restrict__ lno, const uint32_t* __restrict__ perm,
+                                                     int64_t n, uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = lno[perm[i]];
+}
+
+// off[l] = first sorted position whose list is >= l, for l in [0, nlist]
+__global__ __launch_bounds__(256) void k_list_offsets(const uint32_t* __restrict__ sorted, int64_t n, int nlist,
+                                                      int64_t* __restrict__ off) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i > n) return;
+  const int64_t prev = i == 0 ? -1 : (int64_t)sorted[i - 1];
+  const int64_t cur = i == n ? (int64_t)nlist + 1 : (int64_t)sorted[i];
+  for (int64_t l = prev + 1; l <= cur && l <= nlist; l++) off[l] = i;
+}
+
+// entry i of the new image <- source perm[i] (old image below n_old, new entries above)
+__global__ __launch_bounds__(256) void k_gather_entries(const uint32_t* __restrict__ perm, int64_t n, int M,
+                                                        const uint8_t* __restrict__ old_codes, int64_t n_old,
+                                                        const uint8_t* __restrict__ new_codes,
+                                                        const int64_t* __restrict__ ids_all,
+                                                        uint8_t* __restrict__ codes, int64_t* __restrict__ ids) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t src = perm[i];
+  const uint8_t* s = src < n_old ? old_codes + src * M : new_codes + (src - n_old) * M;
+  uint8_t* d = codes + i * M;
+  if ((M & 15) == 0) {
+    for (int v = 0; v < M / 16; v++) reinterpret_cast<uint4*>(d)[v] = reinterpret_cast<const uint4*>(s)[v];
+  } else if ((M & 7) == 0) {
+    for (int v = 0; v < M / 8; v++) reinterpret_cast<uint2*>(d)[v] = reinterpret_cast<const uint2*>(s)[v];
+  } else {
+    for (int v = 0; v < M; v++) d[v] = s[v];
+  }
+  ids[i] = ids_all[src];
+}
+
+int key_bits(int nlist) {
+  int b = 1;
+  while ((1ll << b) <= (int64_t)nlist) b++;
+  return b;
+}
+
+}  // namespace
+
+size_t image_merge_scratch_bytes(int64_t n_all, int nlist) {
+  // lno (2 x u32), perm (2 x u32), ids_all (i64), sort temp (the larger of the two sorts)
+  size_t t1 = 0, t2 = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, t1, (const int64_t*)nullptr, (int64_t*)nullptr, (const uint32_t*)nullptr,
+                                  (uint32_t*)nullptr, (size_t)n_all, 0, 64);
+  (void)rocprim::radix_sort_pairs(nullptr, t2, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n_all, 0, key_bits(nlist));
+  const size_t a = 256;
+  auto up = [&](size_t b) { return (b + a - 1) / a * a; };
+  return up(4 * n_all) * 4 + up(8 * n_all) * 2 + up(std::max(t1, t2));
+}
+
+hipError_t image_merge_sort(const ImageMergeArgs& g, void* scratch, size_t scratch_bytes, hipStream_t s) {
+  const int64_t n = g.n_old + g.n_new;
+  const size_t al = 256;
+  auto up = [&](size_t b) { return (b + al - 1) / al * al; };
+  char* p = static_cast<char*>(scratch);
+  uint32_t* lno = reinterpret_cast<uint32_t*>(p);
+  p += up(4 * n);
+  uint32_t* lno2 = reinterpret_cast<uint32_t*>(p);
+  p += up(4 * n);
+  uint32_t* perm = reinterpret_cast<uint32_t*>(p);
+  p += up(4 * n);
+  uint32_t* perm2 = reinterpret_cast<uint32_t*>(p);
+  p += up(4 * n);
+  int64_t* ids_all = reinterpret_cast<int64_t*>(p);
+  p += up(8 * n);
+  int64_t* ids_sorted = reinterpret_cast<int64_t*>(p);
+  p += up(8 * n);
+  void* tmp = p;
+  size_t tmp_bytes = scratch_bytes - (size_t)(p - static_cast<char*>(scratch));
+  if (n <= 0) return hipSuccess;
+  // keys: every entry's list (old image: expanded from its offsets; new: assignment)
+  if (g.n_old > 0)
+    hipLaunchKernelGGL(k_expand_lists, dim3((unsigned)std::max(1, g.hi - g.lo)), dim3(256), 0, s, g.old_off, g.lo,
+                       g.hi, lno);
+  if (g.n_new > 0)
+    hipLaunchKernelGGL(k_new_keys, dim3(nblk(g.n_new, 256)), dim3(256), 0, s, g.new_lists, g.n_new, g.lo, g.hi,
+                       g.nlist, lno + g.n_old);
+  hipLaunchKernelGGL(k_concat_ids, dim3(nblk(n, 256)), dim3(256), 0, s, g.old_ids, g.n_old, g.new_ids, g.n_new,
+                     ids_all);
+  hipLaunchKernelGGL(k_iota_u32, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n);
+  // 1) by label, 2) by list (stable): (list, label) order
+  hipError_t e = rocprim::radix_sort_pairs(tmp, tmp_bytes, ids_all, ids_sorted, perm, perm2, (size_t)n, 0, 64, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gather_keys, dim3(nblk(n, 256)), dim3(256), 0, s, lno, perm2, n, lno2);
+  e = rocprim::radix_sort_pairs(tmp, tmp_bytes, lno2, lno, perm2, perm, (size_t)n, 0, key_bits(g.nlist), s);
+  if (e != hipSuccess) return e;
+  // lno: sorted lists; perm: source of every sorted position
+  hipLaunchKernelGGL(k_list_offsets, dim3(nblk(n + 1, 256)), dim3(256), 0, s, lno, n, g.nlist, g.off_out);
+  return hipGetLastError();
+}
+
+hipError_t image_merge_gather(const ImageMergeArgs& g, int64_t n_out, void* scratch, hipStream_t s) {
+  const int64_t n = g.n_old + g.n_new;
+  const size_t al = 256;
+  auto up = [&](size_t b) { return (b + al - 1) / al * al; };
+  char* p = static_cast<char*>(scratch);
+  const uint32_t* perm = reinterpret_cast<const uint32_t*>(p + 2 * up(4 * n));
+  const int64_t* ids_all = reinterpret_cast<const int64_t*>(p + 4 * up(4 * n));
+  if (n_out > 0)
+    hipLaunchKernelGGL(k_gather_entries, dim3(nblk(n_out, 256)), dim3(256), 0, s, perm, n_out, g.M, g.old_codes,
+                       g.n_old, g.new_codes, ids_all, g.codes_out, g.ids_out);
+  return hipGetLastError();
+}
+
+void launch_iota_i64(int64_t* v, int64_t n, int64_t start, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_iota_i64, dim3(nblk(n, 256)), dim3(256), 0, s, v, n, start);
+}
+
+}  // namespace chivf

@@ -26,6 +26,7 @@
 
 #include "ivfpq.h"
 #include "ivfpq_kernels.h"
+#include "ivfpq_build.h"
 
 using namespace chivf;
 
@@ -169,13 +170,21 @@ struct ivfpq_index {
   int64_t next_id = 0;
 
   DevBuf d_cent, d_centT, d_cnorm, d_cb, d_T1, d_codes, d_ids, d_off, d_order;
-  std::vector<int32_t> order_host;
   bool dirty = true;
   hipStream_t stream = nullptr;
   // scratch
   DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
   DevBuf h_D, h_I, h_Iq, h_Dq;  // device staging of the host-buffer entry points
   DevBuf w_cand;                // segment candidates of the large-nlist coarse quantizer
+  // device-side add: the new entries of one add call, and the image merge scratch
+  DevBuf a_lists, a_ids, a_codes, a_scratch, a_off;
+  bool host_stale = false;  // the device image holds entries the host lists lack (device-side adds)
+  // T3 of a batch computed ahead (ivfpq_precompute_tables_device), consumed by the
+  // next preassigned search of exactly those queries
+  DevBuf w_T3pre;
+  const float* pre_x = nullptr;
+  int64_t pre_n = 0;
+  hipEvent_t pre_ev = nullptr;
   // list-major plan workspaces (ivfpq_kernels.h ListPlan)
   DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
   // Stream ordering of the per-handle workspaces: every device search records
@@ -297,12 +306,14 @@ struct ivfpq_index {
     }
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     if (done) (void)hipEventDestroy(done);
+    if (pre_ev) (void)hipEventDestroy(pre_ev);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
   void init_stream() {
     if (!stream) HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     if (!done) HIPCHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    if (!pre_ev) HIPCHECK(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
   }
 
   // ---------------------------------------------------------------- helpers
@@ -398,8 +409,6 @@ struct ivfpq_index {
     // Device image: each list sorted by label (stable).  Results do not depend
     // on the order inside a list, and label-sorted lists let the scan kernels
     // rank candidates by code position instead of loading labels.
-    // (M = 16: each code rotated by its list position, see codes_rotated)
-    const bool rot = codes_rotated(M);
     std::vector<int64_t> perm;
     for (int l = 0; l < nlist; l++) {
       const int64_t n = (int64_t)lids[l].size();
@@ -411,28 +420,11 @@ struct ivfpq_index {
       for (int64_t i = 0; i < n; i++) {
         uint8_t* dst = codes.data() + (off[l] + i) * M;
         const uint8_t* src = lcodes[l].data() + perm[i] * M;
-        if (rot)
-          for (int m = 0; m < M; m++) dst[(m + i) & 15] = src[m];
-        else
-          std::memcpy(dst, src, M);
+        std::memcpy(dst, src, M);
         ids[off[l] + i] = lid[perm[i]];
       }
     }
-    // Scheduling order of the shard's lists: largest first (the list scan takes
-    // items in this order within each kind, so the items that finish last are the
-    // short ones: longest-processing-time-first bounds the persistent grid's tail).
-    {
-      const int nloc = std::max(list_hi - list_lo, 1);
-      std::vector<int32_t> order(nloc);
-      for (int j = 0; j < nloc; j++) order[j] = j;
-      if (list_hi > list_lo)
-        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
-          return lids[list_lo + a].size() > lids[list_lo + b].size();
-        });
-      d_order.ensure(sizeof(int32_t) * nloc);
-      HIPCHECK(hipMemcpyAsync(d_order.p, order.data(), sizeof(int32_t) * nloc, hipMemcpyHostToDevice, stream));
-      order_host = std::move(order);  // kept alive until the copy completes (synchronized below)
-    }
+    set_list_order(off);
     d_codes.ensure(std::max<size_t>(16, codes.size()));
     d_ids.ensure(std::max<size_t>(16, sizeof(int64_t) * ids.size()));
     d_off.ensure(sizeof(int64_t) * off.size());
@@ -445,7 +437,127 @@ struct ivfpq_index {
     dirty = false;
   }
 
+  // The host lists from the device image (after device-side adds), in image
+  // order: each list label-sorted.
+  void sync_host() {
+    if (!host_stale) return;
+    quiesce();
+    std::vector<int64_t> off(nlist + 1);
+    HIPCHECK(hipMemcpy(off.data(), d_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToHost));
+    const int64_t tot = off[nlist];
+    std::vector<uint8_t> codes((size_t)tot * M);
+    std::vector<int64_t> ids((size_t)tot);
+    if (tot) {
+      HIPCHECK(hipMemcpy(codes.data(), d_codes.p, codes.size(), hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(ids.data(), d_ids.p, sizeof(int64_t) * ids.size(), hipMemcpyDeviceToHost));
+    }
+    for (int l = 0; l < nlist; l++) {
+      lids[l].assign(ids.begin() + off[l], ids.begin() + off[l + 1]);
+      lcodes[l].assign(codes.begin() + off[l] * M, codes.begin() + off[l + 1] * M);
+    }
+    host_stale = false;
+  }
+
+  // Device-side add of n vectors (x on the host or the device; ids nullable =
+  // sequential): coarse assignment on the matrix cores (the search's coarse
+  // kernels, top-1), PQ encode, then one merge of the new entries into the
+  // device image (ivfpq_build.hip).  No per-chunk host synchronization.
+  void add_dev(int64_t n, const float* x, bool x_on_device, const int64_t* ids, bool ids_on_device, hipStream_t s) {
+    require(trained, "index is not trained");
+    if (n <= 0) return;
+    upload_lists();  // host-side adds not yet in the image
+    order_after_last(s);
+    quiesce();
+    const int64_t rows = nlist >= kSegmentedNlist ? std::min<int64_t>(n, 1 << 18)
+                                                  : std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
+    a_lists.ensure(sizeof(int64_t) * n);
+    a_codes.ensure((size_t)n * M);
+    a_ids.ensure(sizeof(int64_t) * n);
+    w_D.ensure(sizeof(float) * rows);
+    if (!x_on_device) w_x.ensure(sizeof(float) * rows * d);
+    for (int64_t r0 = 0; r0 < n; r0 += rows) {
+      const int64_t c = std::min(rows, n - r0);
+      const float* xd = x + r0 * d;
+      if (!x_on_device) {
+        HIPCHECK(hipMemcpyAsync(w_x.p, xd, sizeof(float) * c * d, hipMemcpyHostToDevice, s));
+        xd = w_x.as<float>();
+      }
+      coarse_launch(xd, c, 1, w_D.as<float>(), a_lists.as<int64_t>() + r0, s);
+      launch_pq_encode(xd, c, d, d_cent.as<float>(), a_lists.as<int64_t>() + r0, d_cb.as<float>(), M, ksub,
+                       a_codes.as<uint8_t>() + r0 * M, s);
+      HIPCHECK(hipGetLastError());
+      if (!x_on_device) HIPCHECK(hipStreamSynchronize(s));  // w_x is reused by the next chunk's copy
+    }
+    if (!ids) {
+      launch_iota_i64(a_ids.as<int64_t>(), n, next_id, s);
+      next_id += n;
+    } else {
+      HIPCHECK(hipMemcpyAsync(a_ids.p, ids, sizeof(int64_t) * n,
+                              ids_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    }
+    ImageMergeArgs g;
+    g.nlist = nlist;
+    g.lo = list_lo;
+    g.hi = list_hi;
+    g.M = M;
+    g.n_old = ntotal;
+    g.old_off = d_off.as<int64_t>();
+    g.old_ids = d_ids.as<int64_t>();
+    g.old_codes = d_codes.as<uint8_t>();
+    g.n_new = n;
+    g.new_lists = a_lists.as<int64_t>();
+    g.new_ids = a_ids.as<int64_t>();
+    g.new_codes = a_codes.as<uint8_t>();
+    a_off.ensure(sizeof(int64_t) * (nlist + 1));
+    g.off_out = a_off.as<int64_t>();
+    const size_t sb = image_merge_scratch_bytes(ntotal + n, nlist);
+    a_scratch.ensure(sb);
+    HIPCHECK(image_merge_sort(g, a_scratch.p, sb, s));
+    std::vector<int64_t> off(nlist + 1);
+    HIPCHECK(hipMemcpyAsync(off.data(), a_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToHost, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    const int64_t n_out = off[nlist];
+    DevBuf codes2, ids2;
+    codes2.ensure(std::max<size_t>(16, (size_t)n_out * M));
+    ids2.ensure(std::max<size_t>(16, sizeof(int64_t) * n_out));
+    g.codes_out = codes2.as<uint8_t>();
+    g.ids_out = ids2.as<int64_t>();
+    HIPCHECK(image_merge_gather(g, n_out, a_scratch.p, s));
+    d_off.ensure(sizeof(int64_t) * (nlist + 1));
+    HIPCHECK(hipMemcpyAsync(d_off.p, a_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToDevice, s));
+    HIPCHECK(hipStreamSynchronize(s));
+    std::swap(d_codes.p, codes2.p);
+    std::swap(d_codes.bytes, codes2.bytes);
+    std::swap(d_ids.p, ids2.p);
+    std::swap(d_ids.bytes, ids2.bytes);
+    ntotal = n_out;
+    a_lists.release();
+    a_codes.release();
+    a_ids.release();
+    a_scratch.release();
+    set_list_order(off);
+    host_stale = true;
+    dirty = false;
+  }
+
+  // Scheduling order of the shard's lists: largest first (the list scan takes
+  // items in this order within each kind, so the items that finish last are the
+  // short ones: longest-processing-time-first bounds the persistent grid's tail).
+  void set_list_order(const std::vector<int64_t>& off) {
+    const int nloc = std::max(list_hi - list_lo, 1);
+    std::vector<int32_t> order(nloc);
+    for (int j = 0; j < nloc; j++) order[j] = j;
+    if (list_hi > list_lo)
+      std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+        return off[list_lo + a + 1] - off[list_lo + a] > off[list_lo + b + 1] - off[list_lo + b];
+      });
+    d_order.ensure(sizeof(int32_t) * nloc);
+    HIPCHECK(hipMemcpyAsync(d_order.p, order.data(), sizeof(int32_t) * nloc, hipMemcpyHostToDevice, stream));
+    HIPCHECK(hipStreamSynchronize(stream));
+  }
+
   void append(int64_t n, const int64_t* lno, const uint8_t* codes, const int64_t* ids) {
+    sync_host();
     for (int64_t i = 0; i < n; i++) {
       const int64_t l = lno[i];
       require(l >= 0 && l < nlist, "list number out of range");
@@ -515,6 +627,8 @@ struct ivfpq_index {
       w_dis0.ensure(sizeof(float) * qc * np);
     }
     const int G = list_scan_group(M, k);
+    const bool use_pre = preassigned && pre_x == x && pre_n == n;
+    pre_x = nullptr;  // consumed (or stale)
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
       const float* xq = x + q0 * d;
@@ -534,14 +648,18 @@ struct ivfpq_index {
                             d_off.as<int64_t>(), list_lo, list_hi, ip(), false, k, plan, s);
       }
       mark_end(tm, s);
-      if (preassigned) {  // T3 (the coarse launch builds it otherwise)
+      const float* T3 = w_T3.as<float>();
+      if (preassigned && use_pre) {  // T3 computed ahead on another stream
+        HIPCHECK(hipStreamWaitEvent(s, pre_ev, 0));
+        T3 = w_T3pre.as<float>() + q0 * M * ksub;
+      } else if (preassigned) {  // T3 (the coarse launch builds it otherwise)
         const int tt = mark_begin(ST_TABLES, s);
         launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
         mark_end(tt, s);
       }
       ScanArgs a;
       a.T1 = d_T1.as<float>();
-      a.T3 = w_T3.as<float>();
+      a.T3 = T3;
       a.codes = d_codes.as<uint8_t>();
       a.ids = d_ids.as<int64_t>();
       a.list_off = d_off.as<int64_t>();
@@ -564,6 +682,22 @@ struct ivfpq_index {
       HIPCHECK(hipGetLastError());
     }
     mark_done(s);
+  }
+
+  // T3 [n][M][ksub] of the queries x, on stream s, ahead of a preassigned search
+  // of exactly those queries (the shard flow computes it while the probes are
+  // all-gathered); ordered after the handle's previous search, which may still read
+  // the buffer.
+  void tables_dev(int64_t n, const float* x, hipStream_t s) {
+    require(trained, "index is not trained");
+    if (n <= 0) return;
+    order_after_last(s);
+    w_T3pre.ensure(sizeof(float) * (size_t)n * M * ksub);
+    launch_ip_table(x, n, d, d_cb.as<float>(), M, ksub, w_T3pre.as<float>(), s);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipEventRecord(pre_ev, s));
+    pre_x = x;
+    pre_n = n;
   }
 
   void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {
@@ -804,43 +938,19 @@ int ivfpq_add(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids) {
     require(h->trained, "index is not trained");
     if (n <= 0) return;
     require(x != nullptr, "null x");
-    h->quiesce();  // the encode scratch buffers are shared with the search path
-    const int d = h->d, M = h->M;
-    const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)h->nlist * 4)));
-    std::vector<int64_t> lno(rows);
-    std::vector<uint8_t> codes((size_t)rows * M);
-    std::vector<int64_t> seq;
-    h->w_x.ensure(sizeof(float) * rows * d);
-    h->w_xn.ensure(sizeof(float) * rows);
-    h->w_dist.ensure(sizeof(float) * rows * h->nlist);
-    h->w_D.ensure(sizeof(float) * rows);
-    h->w_lno.ensure(sizeof(int64_t) * rows);
-    h->w_codes.ensure((size_t)rows * M);
-    for (int64_t r0 = 0; r0 < n; r0 += rows) {
-      const int64_t c = std::min(rows, n - r0);
-      HIPCHECK(hipMemcpyAsync(h->w_x.p, x + r0 * d, sizeof(float) * c * d, hipMemcpyHostToDevice, h->stream));
-      if (!h->ip()) launch_row_norms(h->w_x.as<float>(), c, d, h->w_xn.as<float>(), h->stream);
-      launch_l2_dist(h->w_x.as<float>(), h->w_xn.as<float>(), c, h->d_cent.as<float>(), h->d_cnorm.as<float>(),
-                     h->nlist, d, h->w_dist.as<float>(), h->stream, h->ip());
-      launch_select_rows(h->w_dist.as<float>(), c, h->nlist, 1, h->w_D.as<float>(), h->w_lno.as<int64_t>(),
-                         h->stream);
-      launch_pq_encode(h->w_x.as<float>(), c, d, h->d_cent.as<float>(), h->w_lno.as<int64_t>(),
-                       h->d_cb.as<float>(), M, h->ksub, h->w_codes.as<uint8_t>(), h->stream);
-      HIPCHECK(hipGetLastError());
-      HIPCHECK(hipMemcpyAsync(lno.data(), h->w_lno.p, sizeof(int64_t) * c, hipMemcpyDeviceToHost, h->stream));
-      HIPCHECK(hipMemcpyAsync(codes.data(), h->w_codes.p, (size_t)c * M, hipMemcpyDeviceToHost, h->stream));
-      HIPCHECK(hipStreamSynchronize(h->stream));
-      const int64_t* idp;
-      if (ids) {
-        idp = ids + r0;
-      } else {
-        seq.resize(c);
-        for (int64_t i = 0; i < c; i++) seq[i] = h->next_id + r0 + i;
-        idp = seq.data();
-      }
-      h->append(c, lno.data(), codes.data(), idp);
-    }
-    if (!ids) h->next_id += n;
+    h->add_dev(n, x, false, ids, false, h->stream);
+  });
+}
+
+int ivfpq_add_device(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids, void* stream) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(h->trained, "index is not trained");
+    if (n <= 0) return;
+    require(x != nullptr, "null x");
+    h->add_dev(n, x, true, ids, true, stream ? (hipStream_t)stream : h->stream);
   });
 }
 
@@ -868,6 +978,7 @@ int ivfpq_reset(ivfpq_index* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     for (auto& v : h->lcodes) v.clear();
     for (auto& v : h->lids) v.clear();
+    h->host_stale = false;
     h->ntotal = 0;
     h->next_id = 0;
     h->dirty = true;
@@ -946,6 +1057,16 @@ int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int
     DeviceGuard g(h->device);
     require(msg != nullptr, "null request message");
     h->serve(msg, msg_len, with_lists, batch_size, dim, nprobe, answer, answer_cap, answer_len);
+  });
+}
+
+int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(n >= 0 && (n == 0 || x != nullptr), "null x");
+    h->tables_dev(n, x, stream ? (hipStream_t)stream : h->stream);
   });
 }
 
@@ -1028,16 +1149,30 @@ int ivfpq_get_codebook(const ivfpq_index* h, float* out) {
   });
 }
 
-int ivfpq_get_list_sizes(const ivfpq_index* h, int64_t* out) {
+int ivfpq_get_list_sizes(const ivfpq_index* ch, int64_t* out) {
   return guarded([&] {
-    check_handle(h);
+    check_handle(ch);
+    auto* h = const_cast<ivfpq_index*>(ch);  // the host lists are a cache of the device image
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    if (h->host_stale) {  // from the device image's offsets (no download of the lists)
+      h->quiesce();
+      std::vector<int64_t> off(h->nlist + 1);
+      HIPCHECK(hipMemcpy(off.data(), h->d_off.p, sizeof(int64_t) * (h->nlist + 1), hipMemcpyDeviceToHost));
+      for (int l = 0; l < h->nlist; l++) out[l] = off[l + 1] - off[l];
+      return;
+    }
     for (int l = 0; l < h->nlist; l++) out[l] = (int64_t)h->lids[l].size();
   });
 }
 
-int ivfpq_get_list(const ivfpq_index* h, int list, uint8_t* codes, int64_t* ids) {
+int ivfpq_get_list(const ivfpq_index* ch, int list, uint8_t* codes, int64_t* ids) {
   return guarded([&] {
-    check_handle(h);
+    check_handle(ch);
+    auto* h = const_cast<ivfpq_index*>(ch);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    h->sync_host();
     require(list >= 0 && list < h->nlist, "list id out of range");
     if (codes) std::memcpy(codes, h->lcodes[list].data(), h->lcodes[list].size());
     if (ids) std::memcpy(ids, h->lids[list].data(), sizeof(int64_t) * h->lids[list].size());
@@ -1075,6 +1210,8 @@ int ivfpq_save(ivfpq_index* h, const char* path) {
   return guarded([&] {
     check_handle(h);
     std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    h->sync_host();
     File f(path, "wb");
     f.w(kMagic, 8);
     int32_t hdr[8] = {h->d, h->nlist, h->M, h->nbits, h->metric, h->nprobe, h->trained ? 1 : 0, 0};

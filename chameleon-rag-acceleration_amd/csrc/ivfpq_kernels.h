@@ -134,9 +134,6 @@ int list_scan_group(int M, int k);  // pairs per work item (G) used for (M, k)
 int list_scan_max_items(int64_t npairs, int nloc, int G);
 int scan_lists_grid(int M, int k);  // persistent grid size for the device (2-3 workgroups per CU by LDS)
 bool scan_supported_M(int M);
-// Device code image layout: true = the code at list position i is stored rotated
-// left by (i & 15) bytes (byte m at (m + i) & 15), as the M = 16 list scan reads it.
-bool codes_rotated(int M);
 // list scan + probe merge; ev_lists (nullable): two events recorded around the list-scan kernel alone
 void launch_scan_lists(const ScanArgs& a, const ListPlan& plan, hipStream_t s, hipEvent_t* ev_lists = nullptr);
 

@@ -7,22 +7,25 @@
 // classify_stages.py:127-136) and on the FPGA (retrieval_accelerator/
 // entire_accelerator_final_SIFT_M16/src/{LUT_construction,ADC}.hpp).
 //
-// Design, four launches per batch:
-//  * k_coarse_fused: per query the nprobe nearest lists (fmaf-chain inner
-//    products, wave-level selection), its T3 table, and in the epilogue the
-//    list-major plan: every (query, probe) pair is bucketed under its list,
-//    the query's first usable probe as kind 0, the others as kind 1;
-//  * k_plan_items: (list, up to G pairs) work item records, kind 0 first;
-//  * k_scan_lists: persistent workgroups; per item the G LUTs
-//    (T1[list] - 2 T3[q], or -T3[q] for IP) are formed in LDS (the LUT never
-//    touches HBM) from rows prefetched into registers during the previous
-//    item, the list's PQ codes are streamed coalesced and every code is summed
-//    from M LDS lookups per query; top-k is fused into the scan (per-wave
-//    candidate queue + DPP wave top-k in registers, admission against the
-//    query's running k-th key shared through atomicMin), so no distance is
-//    ever written to memory;
-//  * k_merge_probes: per query the per-wave partial lists of its probes,
-//    labels looked up for survivors only.
+// Design, four launches per batch (C2):
+//  * k_coarse_gemm: the coarse key tiles on the matrix cores
+//    (v_mfma_f32_16x16x4_f32, ascending k = the oracle's fmaf chain) and, in
+//    the same launch, T3 workgroups (per query and sub-quantizer, Faiss tree
+//    order); nlist >= 8192 uses k_coarse_segtop + k_coarse_select_cand instead
+//    (no [B x nlist] key matrix);
+//  * k_coarse_select: per query the nprobe nearest lists; its epilogue plans
+//    the batch: every (query, probe) pair is bucketed under its list, the
+//    query's first usable probe as kind 0, the others as kind 1;
+//  * k_scan_lists: persistent workgroups that derive their work items (list,
+//    up to G pairs, kind 0 first) from the per-list counts; per item the G
+//    LUTs (T1[list] - 2 T3[q], or -T3[q] for IP) are formed in LDS (the LUT
+//    never touches HBM), the list's PQ codes are streamed coalesced and every
+//    code is summed from M LDS lookups per query; top-k is fused into the scan
+//    (per-wave candidate queue + DPP wave top-k in registers, admission against
+//    the query's running k-th key shared through atomicMin), so no distance is
+//    ever written to memory, only each wave's partial top-k;
+//  * k_merge_probes (k <= 64) / k_merge_big (k > 64): per query the partial
+//    lists of its probes, labels looked up for survivors only.
 // Every fp32 operation follows the oracle's order (oracle/ivfpq_oracle.c,
 // Faiss 1.7.1 AVX order); the library is compiled with -ffp-contract=off and
 // the only FMAs are the explicit fmaf() of the coarse inner product.
@@ -35,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ivfpq_kernels.h"
+#include "ivfpq_diag.h"
 
 namespace chivf {
 
@@ -546,30 +550,6 @@ __device__ __forceinline__ void plan_pair(const ListPlan& pl, int nloc, int64_t 
   if (s < pl.cap) pl.bucket[((int64_t)(l - lo) * 2 + kind) * pl.cap + s] = make_int2(pair, __float_as_int(dis0));
 }
 
-#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS)  // diagnostic builds only (profiles/diag_*.py)
-constexpr int kDiagWG = 1024, kDiagItems = 64, kDiagSlots = 16;
-__device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
-#endif
-#ifdef DIAG_CSTAMPS  // k_coarse_fused phase stamps per (workgroup, wave)
-#define CDIAG(slot)                                                                                  \
-  do {                                                                                               \
-    if (lane == 0 && blockIdx.x < kDiagWG)                                                           \
-      g_diag[((size_t)blockIdx.x * kDiagItems + wave) * kDiagSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#define SDIAG(slot)                                                                                  \
-  do {                                                                                               \
-    if (lane == 0 && blockIdx.x < kDiagWG)                                                           \
-      g_diag[((size_t)blockIdx.x * kDiagItems + 4 + wave) * kDiagSlots + (slot)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define CDIAG(slot) \
-  do {              \
-  } while (0)
-#define SDIAG(slot) \
-  do {              \
-  } while (0)
-#endif
-
 // List-major planning request for the coarse selection's epilogue.
 struct CoarsePlan {
   ListPlan pl;
@@ -803,12 +783,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   const int lane = tid & 63;
   const int wave = tid >> 6;
   CDIAG(0);
-#ifdef DIAG_G_NOT3
-  if ((int)blockIdx.x >= ngemm) return;
-#endif
-#ifdef DIAG_G_NOKEYS
-  if ((int)blockIdx.x < ngemm) return;
-#endif
   if ((int)blockIdx.x >= ngemm) {
     // ---- T3 role: 16 queries x one sub-quantizer (256 entries, one per thread)
     const int tb = blockIdx.x - ngemm;
@@ -844,9 +818,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
         t3.out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
       }
     }
-#ifdef DIAG_CSTAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
     CDIAG(5);
     return;
   }
@@ -876,9 +847,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
       keys[(q0 + i) * nlist + c] = coarse_key(acc[t][r], xn[i], cnv, ip);
     }
   }
-#ifdef DIAG_CSTAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-#endif
   CDIAG(5);
 }
 
@@ -944,9 +912,6 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
       v[u] = c < nlist ? row[c] : kInf;
       m = fminf(m, v[u]);
     }
-#ifdef DIAG_CSTAMPS
-    asm volatile("" ::"v"(m));
-#endif
     SDIAG(1);
     const float T = wave_kth_smallest(m, nprobe, lane);
     SDIAG(2);
@@ -981,9 +946,6 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
   }
   SDIAG(3);
   coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
-#ifdef DIAG_CSTAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-#endif
   SDIAG(5);
 }
 
@@ -1218,45 +1180,6 @@ __device__ __forceinline__ void write_item(const ListPlan& pl, const int64_t* __
   rp[3] = make_int4(r[12], r[13], r[14], r[15]);
 }
 
-#ifdef PLAN_MIX_KINDS  // A/B planning variant (r02: within noise at C2)
-// The items of one list when its first-probe pairs (kind 0: c0 of them) and
-// other pairs (c1) share items: slots 0..c-1 run over the kind-0 bucket, then
-// the kind-1 bucket.  The first ceil(c0 / G) items (every first-probe pair, the
-// free slots filled with other pairs of the list) are scheduled in the first
-// phase; the rest after every list's first phase.
-__device__ __forceinline__ void write_item_mixed(const ListPlan& pl, const int64_t* __restrict__ list_off, int lo,
-                                                 int nloc, int G, int rec, int jj, int phase, int t) {
-  const int c0 = min(pl.cnt[jj], pl.cap), c1 = min(pl.cnt[nloc + jj], pl.cap);
-  const int c = c0 + c1;
-  const int cov = min(c, ((c0 + G - 1) / G) * G);  // slots of the first-phase items
-  const int s0 = (phase ? cov : 0) + t * G;
-  const int cnt = min(G, (phase ? c : cov) - s0);
-  const int64_t l = lo + jj;
-  const int64_t beg = list_off[l];
-  int r[16];
-  r[0] = (int)l;
-  r[1] = cnt;
-  r[2] = (int)(list_off[l + 1] - beg);
-  r[3] = (int)(uint32_t)(uint64_t)beg;
-  r[4] = (int)(uint32_t)((uint64_t)beg >> 32);
-#pragma unroll
-  for (int g = 0; g < 4; g++) {
-    int2 v = make_int2(0, 0);
-    const int sl = s0 + g;
-    if (g < cnt) v = sl < c0 ? pl.bucket[((int64_t)jj * 2) * pl.cap + sl] : pl.bucket[((int64_t)jj * 2 + 1) * pl.cap + sl - c0];
-    r[5 + g] = v.x;
-    r[9 + g] = v.y;
-  }
-  r[13] = phase;
-  r[14] = 0;
-  r[15] = 0;
-  int4* rp = reinterpret_cast<int4*>(pl.recs + (int64_t)rec * 16);
-  rp[0] = make_int4(r[0], r[1], r[2], r[3]);
-  rp[1] = make_int4(r[4], r[5], r[6], r[7]);
-  rp[2] = make_int4(r[8], r[9], r[10], r[11]);
-  rp[3] = make_int4(r[12], r[13], r[14], r[15]);
-}
-#endif
 
 __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
                                                              int nloc, int G) {
@@ -1265,23 +1188,12 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
   const int tid = threadIdx.x;
   // per-list exclusive prefix of the item counts, both kinds, in chunks of 1024 lists
   int ca = 0, cb = 0;
-#ifdef PLAN_LIST_ORDER  // items of a kind in list order (A/B)
-  const int32_t* ord = nullptr;
-#else  // items of a kind by list size, largest first
   const int32_t* ord = pl.order;
-#endif
   for (int j0 = 0; j0 < nloc; j0 += PLAN_T) {
     const int j = j0 + tid;  // rank in the scheduling order
     const int jl = j < nloc ? (ord ? ord[j] : j) : 0;
-#ifndef PLAN_MIX_KINDS  // kind-0 and kind-1 pairs in separate items
     const int a = j < nloc ? (min(pl.cnt[jl], pl.cap) + G - 1) / G : 0;
     const int b = j < nloc ? (min(pl.cnt[nloc + jl], pl.cap) + G - 1) / G : 0;
-#else  // (A/B, r02: within noise at C2) first-phase items: the kind-0 pairs plus kind-1 pairs in their free slots
-    const int c0 = j < nloc ? min(pl.cnt[jl], pl.cap) : 0;
-    const int cc = j < nloc ? c0 + min(pl.cnt[nloc + jl], pl.cap) : 0;
-    const int a = (c0 + G - 1) / G;
-    const int b = (cc - min(cc, a * G) + G - 1) / G;
-#endif
     int ea, eb, ta, tb;
     block_scan2(a, b, ea, eb, ta, tb, ws);
     if (j < nloc) {
@@ -1311,11 +1223,7 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
     else
       hi_i = mid;
   }
-#ifndef PLAN_MIX_KINDS
   write_item(pl, list_off, lo, nloc, G, e, ord ? ord[lo_i] : lo_i, kind, ek - exk[lo_i]);
-#else
-  write_item_mixed(pl, list_off, lo, nloc, G, e, ord ? ord[lo_i] : lo_i, kind, ek - exk[lo_i]);
-#endif
 }
 
 __global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const int64_t* __restrict__ list_off, int lo,
@@ -1365,6 +1273,31 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const in
     }
     write_item(pl, list_off, lo, nloc, G, kind ? T0 + P1 + ek : P0 + ek, my0 + lo_i, kind, ek - exk[lo_i]);
   }
+}
+
+__device__ __forceinline__ uint32_t ukey_of(float v) {
+  return (uint32_t)f2ord(v + 0.0f) ^ 0x80000000u;  // unsigned order == float order (-0 folded)
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// the kk-th smallest (1-based) of the wave's NV x 64 values (0xFFFFFFFF = absent);
+// requires kk <= the number of present values
+template <int NV>
+__device__ __forceinline__ uint32_t wave_kth_u32(const uint32_t (&u)[NV], int kk) {
+  uint32_t lo = 0, hi = 0xFFFFFFFEu;
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int cnt = 0;
+#pragma unroll
+    for (int t = 0; t < NV; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u[t] <= mid));
+    if (cnt >= kk) hi = mid; else lo = mid + 1;
+  }
+  return lo;
 }
 
 // ===================================================== list scan (phase B)
@@ -1534,18 +1467,6 @@ struct Item {
 // across workgroups through global atomicMin (any k real candidates bound the
 // final k-th; a stale read is only a looser bound).
 constexpr int QCAP = 256;  // per-wave candidate queue entries
-
-#ifdef DIAG_STAMPS  // diagnostic builds only (profiles/diag_stamps.py): per-item phase stamps
-#define DIAG(slot, v)                                                                                \
-  do {                                                                                               \
-    if (tid == 0 && blockIdx.x < kDiagWG && it_no < kDiagItems)                                      \
-      g_diag[((size_t)blockIdx.x * kDiagItems + it_no) * kDiagSlots + (slot)] = (uint64_t)(v);        \
-  } while (0)
-#else
-#define DIAG(slot, v) \
-  do {                \
-  } while (0)
-#endif
 
 // ---- fused planning: the list scan derives its work items itself
 // (pl.fused: nloc <= kFusedPlanLists and fewer than 65536 items).  Every
@@ -1756,11 +1677,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       b1[buf][e] = T1l[v];
 #pragma unroll
       for (int g = 0; g < G; g++) {
-#ifdef DIAG_NOT3
-        b3[buf][e][g] = make_float4(g, v, 0, 1);
-#else
         b3[buf][e][g] = t3row(g)[v];
-#endif
       }
     }
   };
@@ -1786,11 +1703,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
     for (int j = 0; j < JB; j++) {
       const int i = j * 256 + wave * 64 + lane;
-#ifdef DIAG_NOCODES
-      for (int v = 0; v < M / 4; v++) cw[j].w[v] = (uint32_t)(i * 0x9E3779B1u + v);
-#else
       cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
-#endif
     }
     // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
 #pragma unroll
@@ -1835,21 +1748,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     int qn[G];  // this wave's queue fills (wave-uniform)
 #pragma unroll
     for (int g = 0; g < G; g++) qn[g] = 0;
-#ifdef DIAG_STAMPS
-    int npush = 0;
-    uint64_t tdrain = 0;
-    uint64_t nbulk = 0, ninsert = 0, ndrain = 0;
-#ifdef DIAG_FINE
-    asm volatile("" ::"v"(bound[0]), "v"(bound[G - 1]));
-    DIAG(6, __builtin_amdgcn_s_memtime());
-#endif
-#endif
 
     // drain the queues into the per-query top-k lists and publish the bounds
     auto drain = [&]() __attribute__((always_inline)) {
-#ifdef DIAG_DRAINCNT
-      ndrain++;
-#endif
       for (int b0 = 0; b0 < QG; b0 += 64) {
         bool any = false;
 #pragma unroll
@@ -1863,9 +1764,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
           const bool p = cw64 < tk[g].tp;
           const uint64_t mk = __ballot(p);
           if (!mk) continue;
-#ifdef DIAG_DRAINCNT
-          const uint64_t tb0 = __builtin_amdgcn_s_memtime();
-#endif
           if constexpr (R == 1) {
             if (k <= 16 && qn[g] - b0 <= 16 && __popcll(mk) > 1)
               kc_row16_merge(tk[g], p ? cw64 : kKcNone, lane);
@@ -1879,11 +1777,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
             else
               tk[g].insert(mk, cw64, lane);
           }
-#ifdef DIAG_DRAINCNT
-          asm volatile("" ::"v"(tk[g].p[0]), "s"(tk[g].tp));
-          const uint64_t tb1 = __builtin_amdgcn_s_memtime() - tb0;
-          if (__popcll(mk) > 1) nbulk += tb1; else ninsert += tb1;
-#endif
           bound[g] = fminf(bound[g], tk[g].td());
         }
       }
@@ -1914,12 +1807,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         }
       }
       const int tn = min(JB, (n - sb + 255) >> 8);  // chunks with codes (wave-uniform)
-#ifdef DIAG_FINE
-      if (sb == 0) {
-        asm volatile("" ::"v"(cw[0].w[0]), "v"(cw[JB - 1].w[0]));
-        DIAG(7, __builtin_amdgcn_s_memtime());
-      }
-#endif
       const bool last_sb = sb + 256 * JB >= n;
       // G keys per code: dis0 + sum_m LUT[m][code_m], sequential in m (the
       // oracle's order); two chunks at a time, their 2 x M LDS gathers
@@ -1944,22 +1831,13 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
           for (int m = 0; m < M; m++) {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-#ifdef DIAG_NOGATHER
-              V v;
-              for (int g = 0; g < G; g++) setc(v, g, __int_as_float(cc[h].byte(m)));
-#else
               const V v = lut[m * 256 + cc[h].byte(m)];
-#endif
 #pragma unroll
               for (int g = 0; g < G; g++) dis[2 * jd + h][g] = dis[2 * jd + h][g] + comp(v, g);
             }
           }
         }
       }
-#ifdef DIAG_NOADMIT
-      asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1]));
-      continue;
-#endif
       if constexpr (R == 1) {
         // A query without a bound gets one from this super-batch: the k-th
         // smallest of the 64 lane minima bounds the final k-th key (those minima
@@ -1978,6 +1856,29 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
             if (T < kInf && lane == 0) {
               atomicMin(&s_wb[g], f2ord(T));
               atomicMin(&pl.tauq[qix[g]], f2ord(T));
+            }
+          }
+        }
+      } else {
+        // k > 64: once the super-batch holds k keys (distinct codes), their k-th
+        // smallest bounds the final k-th key (JB x 64 per wave: k <= 384 at M = 16)
+        if (loose && JB * 64 >= k) {
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (bound[g] != kInf) continue;  // wave-uniform
+            uint32_t u[JB];
+            int nv = 0;
+#pragma unroll
+            for (int j = 0; j < JB; j++) {
+              const bool v = j < tn && sb + j * 256 + wave * 64 + lane < n;
+              u[j] = v ? ukey_of(dis[j][g]) : 0xFFFFFFFFu;
+              nv += __popcll(__builtin_amdgcn_ballot_w64(v));
+            }
+            if (nv < k) continue;
+            const int T = (int)(wave_kth_u32<JB>(u, k) ^ 0x80000000u);  // f2ord of the k-th key
+            if (lane == 0) {
+              atomicMin(&s_wb[g], T);
+              atomicMin(&pl.tauq[qix[g]], T);
             }
           }
         }
@@ -2037,9 +1938,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
                   }
                   qn[g] += __popcll(mk[g]);
                 }
-#ifdef DIAG_STAMPS
-                npush += tj;
-#endif
                 if (loose) {  // a query of the item has no bound yet: get one now
                   stop = j + 1;
                   want = true;
@@ -2053,43 +1951,19 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
           pend = want;
           break;
         }
-#ifdef DIAG_STAMPS
-        const uint64_t td0 = __builtin_amdgcn_s_memtime();
         drain();
-        tdrain += __builtin_amdgcn_s_memtime() - td0;
-#else
-        drain();
-#endif
         t = stop;
       }
       bool queued = false;
 #pragma unroll
       for (int g = 0; g < G; g++) queued = queued || qn[g] > 0;
       if (pend || (last_sb && queued)) {
-#ifdef DIAG_STAMPS
-        const uint64_t td0 = __builtin_amdgcn_s_memtime();
         drain();
-        tdrain += __builtin_amdgcn_s_memtime() - td0;
-#else
-        drain();
-#endif
       }
     }
     DIAG(2, __builtin_amdgcn_s_memtime());
-#ifdef DIAG_STAMPS
-#ifndef DIAG_FINE
-    DIAG(7, tdrain);
-#endif
     DIAG(4, n);
     DIAG(5, ci.cnt | (ci.kind << 8));
-#ifndef DIAG_FINE
-#ifdef DIAG_DRAINCNT
-    DIAG(6, (nbulk & 0xFFFFFF) | ((ninsert & 0xFFFFFF) << 24) | (ndrain << 48));
-#else
-    DIAG(6, npush);
-#endif
-#endif
-#endif
 
     if (nxt >= 0) {  // the next item's fields; with kEarly its first loads start here
       unpack(nrec);
@@ -2105,621 +1979,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     it_no++;
     cur = nxt;
   }
-}
-
-// ===================================================== list scan, M = 16, conflict-free gathers
-// The same work items, candidate queues, admission and partial lists as
-// k_scan_lists; a different LDS image and gather schedule:
-//  * LUT image [j][m]: entry (j, m) of the G interleaved tables sits at
-//    (16 j + m) x sizeof(V).  For G = 4 the 16-byte slot of an entry is m, so a
-//    16-lane group of a ds_read_b128 is conflict-free when its 16 lanes read 16
-//    different m.
-//  * Lane l runs the sub-quantizers of its codes staggered by s = l & 15: at
-//    step t it adds sub-table m = (t - s) mod 16 of its current code.  Every
-//    ds_read_b128 lane group covers the 16 residues of l mod 16, so every group
-//    reads 16 distinct m at every step -- and every code is still summed by one
-//    lane in the oracle's order ((dis0 + L0) + L1) + ... + L15: dis0 is folded
-//    into sub-table 0 when the LUT is built (the same fp32 add), a code starts
-//    with an fma by 0 (keep) and its key is captured by a select at m = 15.
-//  * The device image stores the code at list position i rotated left by
-//    (i & 15) bytes (ivfpq_index.cpp upload_lists), so byte u of the lane's
-//    merged word is the code byte its step u needs: no per-lane byte index.
-//  * The next item's T1/T3 rows are loaded into registers while this item is
-//    scanned; the LUT build is then ALU + LDS stores only.
-constexpr uint64_t kRowLane0 = 0x0001000100010001ull;  // lanes with (lane & 15) == 0
-
-// native vector types for the LUT entries (one ds_read_b{32,64,128} per entry;
-// the HIP float2/float4 structs are copied as pairs of 64-bit loads)
-typedef float nf2 __attribute__((ext_vector_type(2)));
-template <int G>
-struct NatVec {
-  using T = float;
-};
-template <>
-struct NatVec<2> {
-  using T = nf2;
-};
-template <>
-struct NatVec<4> {
-  using T = f4;
-};
-__device__ __forceinline__ float ncomp(f4 v, int g) { return v[g]; }
-__device__ __forceinline__ float ncomp(nf2 v, int g) { return v[g]; }
-__device__ __forceinline__ float ncomp(float v, int) { return v; }
-__device__ __forceinline__ void nset(f4& o, int g, float x) { o[g] = x; }
-__device__ __forceinline__ void nset(nf2& o, int g, float x) { o[g] = x; }
-__device__ __forceinline__ void nset(float& o, int, float x) { o = x; }
-
-// The lane id as a value the compiler cannot see through: the lane masks of a
-// compare network built from it are computed where the network runs instead of
-// being hoisted out of the scan loop into ~100 live SGPRs (a rarely run drain or
-// bound network would otherwise pin them for the whole kernel, and force spills).
-__device__ __forceinline__ int opaque_lane(int l) {
-  asm volatile("" : "+v"(l));
-  return l;
-}
-
-// lanes set in the wave-uniform mask m take b, the others a (one VALU)
-__device__ __forceinline__ float sel_lanes(uint64_t m, float a, float b) {
-  float r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-  return r;
-}
-// 0.0 on the lanes of m, 1.0 elsewhere
-__device__ __forceinline__ float keep_lanes(uint64_t m) {
-  float r;
-  asm("v_cndmask_b32_e64 %0, 1.0, 0, %1" : "=v"(r) : "s"(m));
-  return r;
-}
-
-#ifdef DIAG_STAMPS  // diagnostic builds only (profiles/diag_skew.py): per-item stamps of wave 0
-#define SKEW_STAMP(slot, v)                                                                           \
-  do {                                                                                                \
-    if (tid == 0 && blockIdx.x < kDiagWG && it_no < kDiagItems)                                       \
-      g_diag[((size_t)blockIdx.x * kDiagItems + it_no) * kDiagSlots + (slot)] = (uint64_t)(v);         \
-  } while (0)
-#else
-#define SKEW_STAMP(slot, v) \
-  do {                      \
-  } while (0)
-#endif
-
-// pair p of a LUT entry (ext-vector subranges: no instructions)
-__device__ __forceinline__ nf2 npair(f4 v, int p) { return p == 0 ? v.xy : v.zw; }
-__device__ __forceinline__ nf2 npair(nf2 v, int) { return v; }
-__device__ __forceinline__ nf2 npair(float v, int) { return nf2{v, 0.f}; }
-template <int NP>
-__device__ __forceinline__ float pcomp(const nf2 (&f)[NP], int g) { return f[g >> 1][g & 1]; }
-// f[p] := d[p] on the lanes of the wave-uniform mask m: the lanes' exec bits
-// narrowed around two packed moves (instead of one v_cndmask per float)
-template <int NP>
-__device__ __forceinline__ void capture_pairs(nf2 (&f)[NP], const nf2 (&d)[NP], uint64_t m) {
-  uint64_t sv;
-  if constexpr (NP == 2)
-    asm("s_and_saveexec_b64 %[sv], %[m]\n\t"
-        "v_pk_mov_b32 %[f0], %[d0], %[d0] op_sel:[0,1]\n\t"
-        "v_pk_mov_b32 %[f1], %[d1], %[d1] op_sel:[0,1]\n\t"
-        "s_mov_b64 exec, %[sv]"
-        : [f0] "+v"(f[0]), [f1] "+v"(f[1]), [sv] "=&s"(sv)
-        : [d0] "v"(d[0]), [d1] "v"(d[1]), [m] "s"(m)
-        : "scc");
-  else
-    asm("s_and_saveexec_b64 %[sv], %[m]\n\t"
-        "v_pk_mov_b32 %[f0], %[d0], %[d0] op_sel:[0,1]\n\t"
-        "s_mov_b64 exec, %[sv]"
-        : [f0] "+v"(f[0]), [sv] "=&s"(sv)
-        : [d0] "v"(d[0]), [m] "s"(m)
-        : "scc");
-}
-
-struct SkewItem {
-  int rv;  // lanes 0..15 the record, lanes 21..24 the pairs' queries (k_scan_skew16)
-  __device__ __forceinline__ int l() const { return __builtin_amdgcn_readlane(rv, 0); }
-  __device__ __forceinline__ int cnt() const { return __builtin_amdgcn_readlane(rv, 1); }
-  __device__ __forceinline__ int n() const { return __builtin_amdgcn_readlane(rv, 2); }
-  __device__ __forceinline__ int64_t beg() const {
-    return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
-                     (uint32_t)__builtin_amdgcn_readlane(rv, 3));
-  }
-  __device__ __forceinline__ int pair(int g) const { return __builtin_amdgcn_readlane(rv, 5 + g); }
-  __device__ __forceinline__ float d0(int g) const { return __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g)); }
-  __device__ __forceinline__ int q(int g) const { return __builtin_amdgcn_readlane(rv, 21 + g); }
-};
-
-template <int G, int R>
-__global__ __launch_bounds__(256, 2) void k_scan_skew16(ScanArgs a, ListPlan pl) {
-  constexpr int M = 16;
-  using V = typename NatVec<G>::T;
-  __shared__ __attribute__((aligned(16))) V lut[256 * M];
-  constexpr int QG = QCAP / G;
-  __shared__ float qd[4][QCAP];
-  __shared__ int32_t qi[4][QCAP];
-  __shared__ int32_t s_wb[G];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  // wave-uniform by construction, and provably so for the compiler (an SGPR): the
-  // block loop bounds derived from it stay scalar branches, not exec-masked loops
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k = a.k;
-  const int ip = a.ip;
-  const int nloc = a.list_hi - a.list_lo;
-  if (blockIdx.x == 0)  // the counts were consumed by k_plan_items: zero them for the next batch
-    for (int i = tid; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
-  const int n_items = pl.hdr[0];
-  const uint64_t lanemask_lt = (1ull << lane) - 1;
-  // Static item schedule: round r of the persistent grid takes items
-  // [r grid, (r + 1) grid), workgroup w the item r grid + w in even rounds and
-  // r grid + grid - 1 - w in odd ones (snake order over the largest-first item
-  // list).  No work counter: the item after next is known, so its record and its
-  // queries' bounds are loaded a whole item ahead (a claimed index is only known
-  // when its atomic returns, and that return sits in the in-order vmcnt queue
-  // ahead of every later code load).
-  const int grid = gridDim.x;
-  auto item_at = [&](int r) __attribute__((always_inline)) -> int {
-    const int c = r * grid + ((r & 1) ? grid - 1 - (int)blockIdx.x : (int)blockIdx.x);
-    return c < n_items ? c : -1;
-  };
-
-  // skew constants: byte u of MO[u >> 2] = ((u - s) & 15) << 4 (the offset of the
-  // sub-table lane l reads at step u inside a j row); HI = bytes u >= s
-  const int s = lane & 15;
-  uint32_t MO[4], HI[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    uint32_t w = 0, h = 0;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      w |= (uint32_t)((((4 * q + r) - s) & 15) << 4) << (8 * r);
-      h |= (4 * q + r >= s ? 0xFFu : 0u) << (8 * r);
-    }
-    MO[q] = w;
-    HI[q] = h;
-  }
-  // LUT build mapping: thread = sub-quantizer mb, j groups (tid >> 4) + 16 e
-  const int mb = tid & 15;
-
-  auto fetch_rec = [&](int idx) __attribute__((always_inline)) -> int {
-    return pl.recs[(int64_t)idx * 16 + (lane & 15)];
-  };
-  // An item is its 64-B record in one VGPR (lanes 0..15: l, cnt, n, beg lo/hi,
-  // pair[4], dis0[4], kind; lanes 16..31 a copy, where lanes 21..24 are replaced by
-  // the pairs' queries, pair / nprobe, one lane-parallel division per record).
-  // Fields are read with v_readlane where used, so items hold no SGPRs across the scan.
-  auto fetch = [&](int idx) __attribute__((always_inline)) -> SkewItem {
-    int rv = pl.recs[(int64_t)idx * 16 + (lane & 15)];
-    const int cnt = __builtin_amdgcn_readlane(rv, 1), p0 = __builtin_amdgcn_readlane(rv, 5);
-    const int g = (lane & 15) - 5;
-    if (lane >= 16 && g >= 0 && g < 4) rv = (g < cnt ? rv : p0) / a.nprobe;
-    return SkewItem{rv};
-  };
-  auto qof = [&](const SkewItem& it, int g) __attribute__((always_inline)) { return it.q(g); };
-  // An item's table rows -> registers, in four pieces (piece e: T1 row quarter e
-  // and the G T3 row quarters e; IP has no T1, a T3 row is read and ignored).
-  float4 b1[4], b3[G][4];
-  auto piece = [&](const SkewItem& it, int e) __attribute__((always_inline)) {
-    const float4* T1l = ip ? reinterpret_cast<const float4*>(a.T3 + (int64_t)qof(it, 0) * 4096)
-                           : reinterpret_cast<const float4*>(a.T1 + (int64_t)it.l() * 4096);
-    const int v = mb * 64 + (tid >> 4) + 16 * e;
-#ifdef DIAG_NOTAB  // ablation build: no table traffic (wrong results)
-    b1[e] = make_float4(v, e, 1.f, 2.f);
-    for (int g = 0; g < G; g++) b3[g][e] = make_float4(g, v, 0.f, 1.f);
-    (void)T1l;
-#elif defined(DIAG_T3SMALL)  // ablation build: T3 rows of 128 queries only (L2-resident; wrong results)
-    b1[e] = T1l[v];
-#pragma unroll
-    for (int g = 0; g < G; g++) b3[g][e] = reinterpret_cast<const float4*>(a.T3 + (int64_t)(qof(it, g) & 127) * 4096)[v];
-#else
-    b1[e] = T1l[v];
-#pragma unroll
-    for (int g = 0; g < G; g++) b3[g][e] = reinterpret_cast<const float4*>(a.T3 + (int64_t)qof(it, g) * 4096)[v];
-#endif
-  };
-
-  SkewItem it{0}, nit{0}, pit{0};
-  bool have_pit = false;  // a previous item to write out
-  PackedTopK<R> tk[G];  // the wave's per-pair top-k (of the previous item until it is written out)
-  // each wave's sorted partial list per pair (merged by k_merge_probes), and (wave 0)
-  // the workgroup's k-th keys as the queries' bounds
-  auto write_out = [&](const SkewItem& w) __attribute__((always_inline)) {
-    const int wcnt = w.cnt();
-    const int64_t wbeg = w.beg();
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      if (g >= wcnt) continue;
-      write_partial<R>(pl, tk[g], (int64_t)w.pair(g) * 4 + wave, k, wbeg, lane);
-      if (wave == 0 && lane == 0) {
-        const int32_t wb = s_wb[g];
-        if (wb != f2ord(kInf)) atomicMin(&pl.tauq[qof(w, g)], wb);
-      }
-    }
-  };
-  int cur = item_at(0), nxt = item_at(1);
-  if (cur >= 0) {
-    it = fetch(cur);
-#ifndef SKEW_NOPF
-#pragma unroll
-    for (int e = 0; e < 4; e++) piece(it, e);
-#endif
-  }
-  if (nxt >= 0) nit = fetch(nxt);
-  int round = 0;
-
-  int it_no = 0;
-  (void)it_no;
-  while (cur >= 0) {
-    SKEW_STAMP(0, __builtin_amdgcn_s_memtime());
-    __syncthreads();  // (A) every wave is done with the LUT of the previous item and has read s_idx
-    SKEW_STAMP(1, __builtin_amdgcn_s_memtime());
-    // this item's first code words: in flight during the LUT build
-    const int n = it.n();
-    const int lw = wave * 64 + lane;
-    const int nl = n > lw ? (n - lw + 255) >> 8 : 0;
-    const uint4* lc = reinterpret_cast<const uint4*>(a.codes + it.beg() * M);
-#ifdef DIAG_NOCODE  // ablation build: no code traffic (wrong results)
-    auto ldc = [&](int c) __attribute__((always_inline)) -> uint4 {
-      const uint32_t x = (uint32_t)(lw + 256 * c) * 2654435761u;
-      return make_uint4(x, x * 7u, x ^ 0x5555u, x + (uint32_t)(size_t)lc);
-    };
-#else
-    auto ldc = [&](int c) __attribute__((always_inline)) -> uint4 { return lc[c < nl ? lw + 256 * c : 0]; };
-#endif
-    uint4 R4[4];
-    R4[0] = ldc(0);
-    R4[1] = ldc(1);
-    R4[2] = make_uint4(0u, 0u, 0u, 0u);
-    R4[3] = make_uint4(0u, 0u, 0u, 0u);
-    // The previous item's global writes, issued behind this item's first code loads
-    // (vector-memory ops complete in order: stores and atomics issued before a load
-    // would delay every wait for that load): each wave's partial lists, and the
-    // workgroup's bounds (the LDS minimum over its waves) into tau_q.
-    if (have_pit) write_out(pit);
-    const int icnt = it.cnt();
-    // the queries' current bounds (first used after the first super-batch)
-    int tq[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) tq[g] = pl.tauq[qof(it, g)];
-#ifdef SKEW_NOPF  // A/B: this item's rows loaded here, consumed by the build
-#pragma unroll
-    for (int e = 0; e < 4; e++) piece(it, e);
-#endif
-    // LUT = T1 - 2 T3 (L2) or -T3 (IP), with dis0 folded into sub-table 0:
-    // fma(x3, -2, T1) rounds like T1 + (-2 x3) (the product is exact), and
-    // fma(d0, 1, lv) like d0 + lv, fma(d0, 0, lv) = lv.  Entries of absent pairs
-    // are never admitted (their bound is -inf): left as they come.
-    const float f0 = mb == 0 ? 1.f : 0.f;
-    float d0[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) d0[g] = it.d0(g);
-    auto build = [&](auto ipc) __attribute__((always_inline)) {
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const int jg = (tid >> 4) + 16 * e;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          V o;
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            const float x3 = comp(b3[g][e], c);
-            const float lv = decltype(ipc)::value ? -x3 : __builtin_fmaf(x3, -2.f, comp(b1[e], c));
-            nset(o, g, __builtin_fmaf(d0[g], f0, lv));
-          }
-          lut[(4 * jg + c) * 16 + mb] = o;
-        }
-      }
-    };
-#ifndef DIAG_NOBUILD  // ablation build: LUT left as is (wrong results)
-    if (ip)
-      build(std::true_type{});
-    else
-      build(std::false_type{});
-#else
-    asm volatile("" ::"v"(b1[0].x), "v"(b3[G - 1][3].w));
-#endif
-    if (tid < G) s_wb[tid] = f2ord(kInf);
-    __syncthreads();  // (B) the LUT and s_wb are visible
-    SKEW_STAMP(2, __builtin_amdgcn_s_memtime());
-    // the item after next: its record, in flight during this item's scan
-    const int nxt2 = item_at(round + 2);
-    const SkewItem nrec = fetch(nxt2 >= 0 ? nxt2 : cur);
-
-    float bound[G];
-    bool loose = false;  // some query of the item has no bound yet
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      bound[g] = g < icnt ? ord2f(tq[g]) : -kInf;
-      loose = loose || bound[g] == kInf;
-    }
-#pragma unroll
-    for (int g = 0; g < G; g++) tk[g].init(k);
-    int qn[G];  // this wave's queue fills (wave-uniform)
-#pragma unroll
-    for (int g = 0; g < G; g++) qn[g] = 0;
-
-#ifdef DIAG_STAMPS
-    uint64_t d_ndrain = 0, d_tdrain = 0, d_npush = 0, d_nany = 0, d_nloose = 0;
-#endif
-    // drain the queues into the per-query top-k lists and publish the bounds
-    auto drain = [&]() __attribute__((always_inline)) {
-      const int lane = opaque_lane(threadIdx.x & 63);
-#ifdef DIAG_STAMPS
-      d_ndrain++;
-      const uint64_t td0 = __builtin_amdgcn_s_memtime();
-#endif
-      for (int b0 = 0; b0 < QG; b0 += 64) {
-        bool any = false;
-#pragma unroll
-        for (int g = 0; g < G; g++) any = any || b0 < qn[g];
-        if (!any) break;
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          if (b0 >= qn[g]) continue;
-          const int e = b0 + lane;
-          const uint64_t cw64 = e < qn[g] ? pack_kc(qd[wave][g * QG + e], qi[wave][g * QG + e]) : kKcNone;
-          const bool p = cw64 < tk[g].tp;
-          const uint64_t mk = __ballot(p);
-          if (!mk) continue;
-          if constexpr (R == 1) {
-#ifdef SKEW_ONEMERGE
-            kc_bulk_merge(tk[g], p ? cw64 : kKcNone, lane);
-#else
-            if (k <= 16 && qn[g] - b0 <= 16 && __popcll(mk) > 1)
-              kc_row16_merge(tk[g], p ? cw64 : kKcNone, lane);
-            else if (__popcll(mk) > 4)
-              kc_bulk_merge(tk[g], p ? cw64 : kKcNone, lane);
-            else
-              tk[g].insert(mk, cw64, lane);
-#endif
-          } else {
-            if (__popcll(mk) > 4)
-              kc_bulk_merge_rows(tk[g], p ? cw64 : kKcNone, lane);
-            else
-              tk[g].insert(mk, cw64, lane);
-          }
-          bound[g] = fminf(bound[g], tk[g].td());
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < G; g++) qn[g] = 0;
-      loose = false;
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        loose = loose || bound[g] == kInf;
-        if (g < icnt && tk[g].tp != kKcNone && lane == 0) atomicMin(&s_wb[g], f2ord(tk[g].td()));
-      }
-#ifdef DIAG_STAMPS
-      asm volatile("" ::"v"(tk[0].p[0]), "s"(tk[G - 1].tp));
-      d_tdrain += __builtin_amdgcn_s_memtime() - td0;
-#endif
-    };
-
-    // Lane's codes: list positions lw + 256 c, c < nl.  Blocks b = 0 .. cmax of 16
-    // steps (block b adds sub-tables m >= 0 of code b and finishes code b - 1 for
-    // s > 0; the last block only finishes codes), four per super-batch.  The code
-    // words sit in a ring R[c & 3] (static register indices, no copies that would
-    // wait for loads in flight); code b + 2 is loaded during block b.  Codes past
-    // the lane's last one are clamped loads of a valid code: their keys are never
-    // admitted, so their bytes do not matter.
-    const int cmax = n > wave * 64 ? (n - wave * 64 + 255) >> 8 : 0;  // wave-uniform (lane 0 has the most)
-    const int nblk = cmax > 0 ? cmax + 1 : 0;
-    // running keys in pairs (v_pk_fma_f32: two queries per instruction)
-    constexpr int NP = (G + 1) / 2;
-    nf2 dp[NP];
-#pragma unroll
-    for (int p = 0; p < NP; p++) dp[p] = nf2{0.f, 0.f};
-
-#ifdef DIAG_STAMPS
-    uint64_t t_gather = 0;
-#endif
-    for (int sb = 0; sb < nblk; sb += 4) {
-#ifdef DIAG_STAMPS
-      const uint64_t tg0 = __builtin_amdgcn_s_memtime();
-#endif
-      nf2 fp[4][NP];  // the keys each lane finished, per block
-      const int tn = min(4, nblk - sb);  // blocks in this super-batch (wave-uniform)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (j < tn) {
-          const int b = sb + j;
-          // bytes u >= s from code b, bytes u < s from code b - 1
-          uint32_t W[4];  // ((a ^ b) & m) ^ b: one v_bfi_b32 per word
-          W[0] = ((R4[j].x ^ R4[(j + 3) & 3].x) & HI[0]) ^ R4[(j + 3) & 3].x;
-          W[1] = ((R4[j].y ^ R4[(j + 3) & 3].y) & HI[1]) ^ R4[(j + 3) & 3].y;
-          W[2] = ((R4[j].z ^ R4[(j + 3) & 3].z) & HI[2]) ^ R4[(j + 3) & 3].z;
-          W[3] = ((R4[j].w ^ R4[(j + 3) & 3].w) & HI[3]) ^ R4[(j + 3) & 3].w;
-          R4[(j + 2) & 3] = ldc(b + 2);
-#ifndef SKEW_NOPF
-          if (sb == 0 && nxt >= 0) piece(nit, j);  // the next item's rows, spread over the first blocks
-#endif
-#ifdef DIAG_STAMPS
-          if (b == 0) {
-            asm volatile("" ::"v"(W[0]), "v"(W[3]));
-            SKEW_STAMP(3, __builtin_amdgcn_s_memtime());
-          }
-#endif
-          // the block's lookups are independent of the sums: kept LA steps ahead
-#ifndef SKEW_LA
-#define SKEW_LA 8
-#endif
-          constexpr int LA = SKEW_LA;
-          V v[16];
-          auto lookup = [&](int u) __attribute__((always_inline)) {
-            const int r = u & 3;
-            // (j << 8) | (m << 4) = 16 x entry index (16 j + m); a typed load of V
-            // (the entry's alignment comes from its type)
-            const uint32_t a16 =
-                __builtin_amdgcn_perm(W[u >> 2], MO[u >> 2], 0x0C0C0000u | ((4u + r) << 8) | (uint32_t)r);
-            v[u] = *reinterpret_cast<const V*>(reinterpret_cast<const char*>(lut) + (a16 >> (G == 4 ? 0 : G == 2 ? 1 : 2)));
-          };
-#pragma unroll
-          for (int u = 0; u < LA; u++) lookup(u);
-          // lanes with s == u (their m is 0) and s == u + 1 (m is 15): one SGPR
-          // pair shifted per step (opaque, so that 16 constant pairs are not held)
-          uint64_t m0 = kRowLane0;
-#pragma unroll
-          for (int u = 0; u < 16; u++) {
-            if (u + LA < 16) lookup(u + LA);
-            asm volatile("" : "+s"(m0));
-            const uint64_t m15 = u == 15 ? kRowLane0 : m0 << 1;
-            const float keep = keep_lanes(m0);
-            const nf2 kk = nf2{keep, keep};
-#pragma unroll
-            for (int p = 0; p < NP; p++) dp[p] = __builtin_elementwise_fma(dp[p], kk, npair(v[u], p));
-            if (u == 0)
-#pragma unroll
-              for (int p = 0; p < NP; p++) fp[j][p] = dp[p];  // (lanes with s = 1 finish here)
-            capture_pairs<NP>(fp[j], dp, m15);
-            m0 = m15;
-          }
-        }
-      }
-#ifdef DIAG_STAMPS
-      asm volatile("" ::"v"(fp[0][0]), "v"(fp[3][NP - 1]));
-      t_gather += __builtin_amdgcn_s_memtime() - tg0;
-#endif
-#ifdef DIAG_NOADMIT  // ablation build: no admission (wrong results)
-      asm volatile("" ::"v"(fp[0][0]), "v"(fp[1][0]), "v"(fp[2][0]), "v"(fp[3][0]));
-      continue;
-#endif
-      // the codes the lanes finished in this super-batch: c = b (s == 0) or b - 1
-      bool valid[4];
-      int pos[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const int cf = s == 0 ? sb + j : sb + j - 1;
-        valid[j] = j < tn && cf >= 0 && cf < nl;
-        pos[j] = lw + 256 * cf;
-      }
-      const bool last_sb = sb + 4 >= nblk;
-#ifndef DIAG_NOLOOSE
-      if constexpr (R == 1) {
-        // A query without a bound gets one from this super-batch: the k-th smallest
-        // of the lane minima (distinct codes) bounds the final k-th key; shared with
-        // the other waves (LDS) and workgroups (tau_q).
-        if (loose) {
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            if (bound[g] != kInf) continue;  // wave-uniform
-            float mn = kInf;
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-              if (valid[j]) mn = fminf(mn, pcomp(fp[j], g));
-            const float T = wave_kth_smallest(mn, k, opaque_lane(threadIdx.x & 63));
-            if (T < kInf && lane == 0) atomicMin(&s_wb[g], f2ord(T));
-          }
-        }
-      }
-#endif
-      loose = false;
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        if (g < icnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));
-        loose = loose || bound[g] == kInf;
-      }
-      // Admission, block by block: a straight sequence of guarded blocks (static
-      // register indices) that stops where the queue needs draining; one drain site.
-      int t = 0;
-      bool pend = false;  // a drain requested by the last block
-      bool anyc = false;
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-#pragma unroll
-        for (int g = 0; g < G; g++) anyc = anyc || (valid[j] && pcomp(fp[j], g) <= bound[g]);
-      if (__builtin_amdgcn_ballot_w64(anyc) == 0) t = 4;  // nothing to admit in this super-batch
-#ifdef DIAG_NOPUSH
-      t = 4;
-      asm volatile("" ::"v"((int)anyc));
-#endif
-#ifdef DIAG_STAMPS
-      if (t == 0) d_nany++;
-      if (loose) d_nloose++;
-#endif
-      while (t < 4) {
-        int stop = 4;       // first block not yet admitted
-        bool want = false;  // drain requested
-        bool go = true;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          if (go && j >= t) {  // wave-uniform
-            uint64_t mk[G];
-            int tj = 0;
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              mk[g] = __builtin_amdgcn_ballot_w64(valid[j] && pcomp(fp[j], g) <= bound[g]);
-              tj += __popcll(mk[g]);
-            }
-            bool full = false;
-#pragma unroll
-            for (int g = 0; g < G; g++) full = full || qn[g] + __popcll(mk[g]) > QG;
-            if (tj > 0) {
-              if (full) {  // no room: drain first, then redo this block
-                stop = j;
-                want = true;
-                go = false;
-              } else {
-#pragma unroll
-                for (int g = 0; g < G; g++) {
-                  if ((mk[g] >> lane) & 1) {
-                    const int sl = g * QG + qn[g] + __popcll(mk[g] & lanemask_lt);
-                    qd[wave][sl] = pcomp(fp[j], g);
-                    qi[wave][sl] = pos[j];
-                  }
-                  qn[g] += __popcll(mk[g]);
-#ifdef DIAG_STAMPS
-                  d_npush += __popcll(mk[g]);
-#endif
-                }
-                if (loose) {  // a query of the item has no bound yet: get one now
-                  stop = j + 1;
-                  want = true;
-                  go = false;
-                }
-              }
-            }
-          }
-        }
-        if (stop >= 4) {  // a drain wanted here is left to the end of the super-batch
-          pend = want;
-          break;
-        }
-        drain();
-        t = stop;
-      }
-      bool queued = false;
-#pragma unroll
-      for (int g = 0; g < G; g++) queued = queued || qn[g] > 0;
-      if (pend || (last_sb && queued)) drain();
-    }
-#ifndef SKEW_NOPF
-    // waves without codes: the next item's rows in full; short items: the pieces not yet issued
-    if (nxt >= 0)
-#pragma unroll
-      for (int e = 0; e < 4; e++)
-        if (e >= nblk) piece(nit, e);
-#endif
-    SKEW_STAMP(4, __builtin_amdgcn_s_memtime());
-#ifdef DIAG_STAMPS
-    SKEW_STAMP(7, t_gather);
-    SKEW_STAMP(8, d_ndrain);
-    SKEW_STAMP(9, d_tdrain);
-    SKEW_STAMP(10, d_npush);
-    SKEW_STAMP(11, d_nany | (d_nloose << 16));
-#endif
-    // waves without codes: the next item's rows in full; short items: the pieces not yet issued
-
-    pit = it;
-    have_pit = true;
-    SKEW_STAMP(5, __builtin_amdgcn_s_memtime());
-    SKEW_STAMP(6, (uint32_t)it.n() | ((uint64_t)__builtin_amdgcn_readlane(it.rv, 13) << 32) | ((uint64_t)it.cnt() << 40) | ((uint64_t)nblk << 48));
-    it_no++;
-    it = nit;
-    cur = nxt;
-    nxt = nxt2;
-    if (nxt2 >= 0) nit = nrec;
-    round++;
-  }
-  __syncthreads();  // s_wb holds the last item's final bounds
-  if (have_pit) write_out(pit);
 }
 
 // ------------------------------------------- large-nlist coarse (no key matrix)
@@ -2999,31 +2258,6 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
 // pass2SelectLists (classify_stages.py:127-136; 78 % of the time at K = 1000,
 // MICRO_GPU_profiling/out_img/profile_experiment_5_topK.png).
 constexpr int kBigCap = 2048;
-
-__device__ __forceinline__ uint32_t ukey_of(float v) {
-  return (uint32_t)f2ord(v + 0.0f) ^ 0x80000000u;  // unsigned order == float order (-0 folded)
-}
-
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// the kk-th smallest (1-based) of the wave's NV x 64 values (0xFFFFFFFF = absent);
-// requires kk <= the number of present values
-template <int NV>
-__device__ __forceinline__ uint32_t wave_kth_u32(const uint32_t (&u)[NV], int kk) {
-  uint32_t lo = 0, hi = 0xFFFFFFFEu;
-  while (lo < hi) {
-    const uint32_t mid = lo + ((hi - lo) >> 1);
-    int cnt = 0;
-#pragma unroll
-    for (int t = 0; t < NV; t++) cnt += __popcll(__builtin_amdgcn_ballot_w64(u[t] <= mid));
-    if (cnt >= kk) hi = mid; else lo = mid + 1;
-  }
-  return lo;
-}
 
 __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   constexpr int SV = 20;  // sample slots per lane
@@ -3408,7 +2642,7 @@ void launch_plan_count(const int64_t* lists, const float* Dq, const float* x, co
 }
 
 bool scan_fused_plan(int nloc, int max_items, int M) {
-  return nloc <= kFusedPlanLists && max_items < 65536 && !codes_rotated(M);
+  return nloc <= kFusedPlanLists && max_items < 65536 && M > 0;
 }
 
 void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int hi, int G, hipStream_t s) {
@@ -3423,21 +2657,13 @@ void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int 
 }
 
 bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 || M == 64; }
-#ifndef SCAN_SKEW16
-#define SCAN_SKEW16 0  // 1: M = 16 by k_scan_skew16 over rotated codes (r03 A/B: 144 vs 120 us, kept off)
-#endif
-bool codes_rotated(int M) { return SCAN_SKEW16 && M == 16; }
-
-#ifndef SCAN_G_MAX
-#define SCAN_G_MAX 4  // pairs per work item (A/B builds may lower it)
-#endif
 // Pairs per work item: G LUTs of M x 256 floats interleaved in LDS (<= 64 KB),
 // G x R <= 8 (the per-wave top-k state).  For k > 64 at M <= 16, G = 2 and three
 // workgroups per CU beat G = 4 with two (k = 100 at C2: 174 vs 225 us, r02 A/B).
 constexpr int scan_group(int M, int R) {
-  return (SCAN_G_MAX >= 4 && M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16)) ? 4
-         : (SCAN_G_MAX >= 2 && M * 1024 * 2 <= 65536 && 2 * R <= 8)                      ? 2
-                                                                                          : 1;
+  return (M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16)) ? 4
+         : (M * 1024 * 2 <= 65536 && 2 * R <= 8)                      ? 2
+                                                                      : 1;
 }
 int list_scan_group(int M, int k) {
   const int R = rows_for(k);
@@ -3463,32 +2689,20 @@ int scan_lists_grid(int M, int k) {
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     cus = n;
   }
-#ifdef SCAN_WG_PER_CU
-  const int per_cu = SCAN_WG_PER_CU;
-#else
-  // workgroups per CU the LDS allows (LUTs + candidate queues), at most 3
+  // workgroups per CU the LDS allows (LUTs, candidate queues, fused-plan prefix), at most 3
   const int lds = M * 256 * 4 * list_scan_group(M, k) + 4 * QCAP * 8 + 6 * kFusedPlanLists + 96;
   const int per_cu = std::max(1, std::min(3, 160 * 1024 / lds));
-#endif
   return std::max(8, (per_cu * cus + 7) / 8 * 8);
 }
 
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
-#ifndef SCAN_JB16
-#define SCAN_JB16 6  // r02 A/B at C2: 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
-#endif
-  constexpr int JB = M <= 16 ? SCAN_JB16 : M <= 32 ? 4 : 2;  // code chunks held in registers per item (32 VGPRs), even
+  // code chunks held in registers per item (32 VGPRs), even; r02 A/B at C2 M = 16:
+  // 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
+  constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : 2;
   if (ev) (void)hipEventRecord(ev[0], s);
-  if constexpr (M == 16 && SCAN_SKEW16)  // rotated device codes (codes_rotated(16)): the conflict-free scan
-    hipLaunchKernelGGL((k_scan_skew16<G, R>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
-  else
-    hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
-#ifdef SCAN_TWICE  // diagnostic build only: re-scan with every query's tau already tight
-  (void)hipMemsetAsync(pl.hdr + 2, 0, sizeof(int32_t), s);
   hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
-#endif
   if (ev) (void)hipEventRecord(ev[1], s);
   if (R >= 2 && a.nprobe <= 64) hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);

@@ -498,6 +498,31 @@ class IndexIVFPQ:
             D.data_ptr(), I.data_ptr(), ctypes.c_void_p(self._stream(x, stream))))
         return D, I
 
+    def precompute_tables_device(self, x, stream=None):
+        """T3 of the queries x (torch CUDA [n, d]) on ``stream``, for the next
+        search_preassigned_device of exactly this tensor: the shard flow runs it
+        on a side stream while the coarse step and the probe all-gather run."""
+        import torch
+
+        n = x.shape[0] if x.dim() == 2 else -1
+        self._check_dev(x, "x", torch.float32, (n, self.d))
+        _lib.check(_lib.load().ivfpq_precompute_tables_device(self._h, n, x.data_ptr(),
+                                                              ctypes.c_void_p(self._stream(x, stream))))
+
+    def add_device(self, x, ids=None, stream=None):
+        """add / add_with_ids with the vectors already in HBM (torch float32 CUDA
+        tensor [n, d]; ids: int64 CUDA tensor [n] or None for sequential ids).
+        Assignment, encoding and the list-image merge run on the GPU; returns
+        once the new image is in place."""
+        import torch
+
+        n = x.shape[0] if x.dim() == 2 else -1
+        self._check_dev(x, "x", torch.float32, (n, self.d))
+        if ids is not None:
+            self._check_dev(ids, "ids", torch.int64, (n,))
+        _lib.check(_lib.load().ivfpq_add_device(self._h, n, x.data_ptr(), ids.data_ptr() if ids is not None else None,
+                                                ctypes.c_void_p(self._stream(x, stream))))
+
     def coarse_device(self, x, Iq=None, Dq=None, stream=None):
         """The coarse quantizer alone: (Dq, Iq) [n, min(nprobe, nlist)] -- L2
         distances ascending or inner products descending."""

@@ -54,6 +54,14 @@ int ivfpq_train(ivfpq_index* h, int64_t n, const float* x, int niter_coarse, int
  * ids == NULL assigns ntotal, ntotal+1, ...  Encoding runs on the GPU. */
 int ivfpq_add(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids);
 
+/* Index.add / add_with_ids with the vectors (and ids, nullable) already in HBM:
+ * device pointers, on `stream` (NULL = the handle's stream).  Coarse assignment
+ * on the matrix cores (the search's coarse kernels, top-1), PQ encode and the
+ * merge into the device list image all run on the GPU (ivfpq_add takes the same
+ * path from host buffers).  Reference: bench_gpu_1bn.py:598-658 (the 1e9 base
+ * set added through the GPU index in slices).  Returns when the image is in place. */
+int ivfpq_add_device(ivfpq_index* h, int64_t n, const float* x, const int64_t* ids, void* stream);
+
 /* invlists.add_entries with precomputed (list, code, id) triples, e.g. from a
  * loaded Faiss index or another shard.  codes: uint8 [n][M]. */
 int ivfpq_add_preencoded(ivfpq_index* h, int64_t n, const int64_t* list_no, const uint8_t* codes,
@@ -100,6 +108,14 @@ int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, i
  * (decode_request_with_lists asserts, serialization_utils.py:211-213). */
 int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int with_lists, int batch_size, int dim,
                         int nprobe, uint8_t* answer, int64_t answer_cap, int64_t* answer_len);
+
+/* The inner-product tables T3 of n HBM-resident queries, computed on `stream`
+ * ahead of a search_preassigned_device of exactly those queries (same pointer
+ * and n), which then uses them instead of building its own.  The shard flow
+ * issues it on a side stream while the coarse step and the probe all-gather run
+ * (T3 depends only on the queries).  Reference: IndexIVFPQ::search_preassigned's
+ * per-query precompute_list_tables (bench_gpu_1bn.py:605-616 shard step). */
+int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream);
 
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing

@@ -4,9 +4,10 @@ global batch of 1024 x N queries.
 
   coarse   : coarse_device on the rank's own 1024-query slice (flat in N)
   preassigned: search_preassigned_device of the whole batch on the rank's lists
-               (plan + T3 tables for the batch + scan + merge), with its stage
-               split (ms): tables (T3, grows with the batch), scan (flat: the
-               rank's lists see B x nprobe pairs on average)
+               (plan + scan + merge; T3 for the batch is computed on a side stream
+               concurrently with the coarse step, as bench.py does), with the stage
+               split of a run without the side stream (ms): tables (T3, grows with
+               the batch), scan
   merge    : merge_topk_device of the rank's slice over N partials
 
 Collectives are not run (one GPU): their per-rank bytes are printed instead
@@ -60,9 +61,13 @@ def main():
         xg = xd[:N * B]
         Dq_all, Iq_all = full.coarse_device(xg)  # stands in for the all-gathered probes
         t = {"coarse": 0.0, "preassigned": 0.0, "merge": 0.0}
+        side = torch.cuda.Stream()
         for rep in range(args.reps + 2):
             e = [ev() for _ in range(4)]
             e[0].record()
+            # T3 of the global batch on a side stream, concurrent with the coarse step (bench.py's shard flow)
+            side.wait_stream(torch.cuda.current_stream())
+            sh.precompute_tables_device(xg, stream=side.cuda_stream)
             sh.coarse_device(xg[:B])
             e[1].record()
             Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all)
