@@ -75,6 +75,9 @@ def parse():
     p.add_argument("--nt", type=int, default=100_000)
     p.add_argument("--nbatches", type=int, default=10)
     p.add_argument("--niter", type=int, default=25)
+    p.add_argument("--centres", type=int, default=200_000,
+                   help="Gaussian centres of the synthetic generator (200k: the recall curve tracks SIFT1M's; "
+                        "rounds 1-2 used 10k)")
     p.add_argument("--mode", choices=["shard", "replicas"], default="shard")
     p.add_argument("--cpu-sample", type=int, default=10240, help="queries in the CPU-baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (repetitions)")
@@ -112,10 +115,11 @@ def main():
     B = args.batch
     Bg = B * world if shard else B  # queries per step on each rank
     log(f"rank {rank}/{world} generating data nb={args.nb} nt={args.nt}")
-    xt = datasets.synthetic_sift_like(args.nt, args.d, seed=4321)
-    xb = datasets.synthetic_sift_like(args.nb, args.d, seed=1234)
+    gen = dict(n_centres=args.centres)
+    xt = datasets.synthetic_sift_like(args.nt, args.d, seed=4321, **gen)
+    xb = datasets.synthetic_sift_like(args.nb, args.d, seed=1234, **gen)
     nq_total = args.nbatches * Bg
-    xq = datasets.synthetic_sift_like(nq_total, args.d, seed=123 + (0 if shard else rank))
+    xq = datasets.synthetic_sift_like(nq_total, args.d, seed=123 + (0 if shard else rank), **gen)
 
     ix = faiss.index_factory(args.d, f"IVF{args.nlist},PQ{args.M}", device=local_rank)
     ix.niter_coarse = ix.niter_pq = args.niter
@@ -310,7 +314,8 @@ def main():
 
     traffic = None
     traffic_src = "no counter file"
-    config_key = f"nb{args.nb}-d{args.d}-IVF{args.nlist}-PQ{args.M}-np{args.nprobe}-k{k}-B{B}-w{world}-{args.mode}"
+    config_key = (f"nb{args.nb}-d{args.d}-IVF{args.nlist}-PQ{args.M}-np{args.nprobe}-k{k}-B{B}-w{world}-{args.mode}"
+                  f"-c{args.centres}")
     sha = lib_sha256()
     if os.path.exists(args.pmc_json):
         try:
@@ -338,8 +343,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SIFT1M-shaped clustered integer-valued float32, seeds base 1234 / train 4321 / "
-                    "queries 123); index trained on the GPU",
+            "data": f"synthetic (SIFT1M-shaped clustered integer-valued float32, {args.centres} centres, sigma 16, "
+                    "seeds base 1234 / train 4321 / queries 123); index trained on the GPU",
             "config": {
                 "workload": f"IVF{args.nlist},PQ{args.M}x8 search, d={args.d}, nb={args.nb}, nprobe={args.nprobe}, "
                             f"k={k}, batch={B} queries per GPU per step",

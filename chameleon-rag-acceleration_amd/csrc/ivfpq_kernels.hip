@@ -850,6 +850,50 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   CDIAG(5);
 }
 
+// T3 on the matrix cores -- a tolerance-mode A/B build only (-DT3_MFMA via
+// profiles/build_variants.sh; never the shipped library).  T3[q][m][j] =
+// <x_q[m], C_mj> as one 16 x 16 v_mfma_f32_16x16x4_f32 tile per (16 queries,
+// 16 codewords), K = dsub: a sequential fma chain over the sub-vector instead
+// of Faiss's 8-wide tree, so the LUT (and the ids of near-ties) can differ from
+// the oracle's.  Workgroup = 16 queries x one sub-quantizer; wave w: codewords
+// 64 w .. 64 w + 63.  profiles/r03_t3_mfma.txt has the A/B.
+#ifdef T3_MFMA
+__global__ __launch_bounds__(256) void k_t3_mfma(const float* __restrict__ x, int64_t nq, int d,
+                                                 const float* __restrict__ cb, int M, float* __restrict__ out) {
+  __shared__ float xs[16 * 16];  // [t][16 queries], t < dsub padded to 4
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int dsub = d / M, dk = (dsub + 3) & ~3;
+  const int64_t q0 = (int64_t)(blockIdx.x / M) * 16;
+  const int m = blockIdx.x % M;
+  for (int e = tid; e < 16 * dk; e += 256) {
+    const int t = e / 16, i = e % 16;
+    xs[e] = (t < dsub && q0 + i < nq) ? x[(q0 + i) * d + m * dsub + t] : 0.f;
+  }
+  __syncthreads();
+  const int i16 = lane & 15, k4 = lane >> 4;
+  f4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < dk; k0 += 4) {
+    const int kk = k0 + k4;
+    const float av = xs[kk * 16 + i16];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int j = wave * 64 + t * 16 + i16;
+      const float bv = kk < dsub ? cb[((int64_t)m * 256 + j) * dsub + kk] : 0.f;
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; t++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int64_t q = q0 + k4 * 4 + r;
+      if (q < nq) out[q * (int64_t)M * 256 + m * 256 + wave * 64 + t * 16 + i16] = acc[t][r];
+    }
+}
+#endif  // T3_MFMA
+
 // Write a query's top-nprobe (run: packed (key, list), ascending across the
 // wave) and, with cp.on, plan its probes for the list-major scan.
 __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, int nprobe, float* __restrict__ out_dis,
@@ -2285,8 +2329,11 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   C = wave_sum_i(C);
   __builtin_amdgcn_wave_barrier();
   uint32_t Tu = 0xFFFFFFFFu;  // every entry is a candidate
-  for (int round = 0; C > kBigCap && round < 8; round++) {
+  bool exact = false;         // Tu is the exact k-th key (a round sampled every entry)
+  const int Cmax = max(2 * k, k + 64);
+  for (int round = 0; C > Cmax && round < 8; round++) {
     const int r = (C + 64 * SV - 1) / (64 * SV);
+    exact = r == 1;
     // exclusive prefix of per-list sample counts (lists in j order: 4 scans of 64)
     int carry = 0;
 #pragma unroll
@@ -2364,19 +2411,29 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // the exact k-th key: keep the k best and their ties (in place, order kept)
-  if (C > k) {
+  if (C > k && !exact) {
+    const int nt = (C + 63) >> 6;  // wave-uniform: rows of the buffer in use
     uint32_t u2[kBigCap / 64];
 #pragma unroll
     for (int t = 0; t < kBigCap / 64; t++) {
       const int e = t * 64 + lane;
-      u2[t] = e < C ? ukey_of(cd[e]) : 0xFFFFFFFFu;
+      u2[t] = (t < nt && e < C) ? ukey_of(cd[e]) : 0xFFFFFFFFu;
     }
-    const uint32_t T2 = wave_kth_u32<kBigCap / 64>(u2, k);
+    uint32_t lo = 0, hi = 0xFFFFFFFEu;
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      int cnt = 0;
+#pragma unroll
+      for (int t = 0; t < kBigCap / 64; t++)
+        if (t < nt) cnt += __popcll(__builtin_amdgcn_ballot_w64(u2[t] <= mid));
+      if (cnt >= k) hi = mid; else lo = mid + 1;
+    }
+    const uint32_t T2 = lo;
     int n2 = 0;
 #pragma unroll
     for (int t = 0; t < kBigCap / 64; t++) {
       const int e = t * 64 + lane;
-      const bool keep = e < C && u2[t] <= T2;
+      const bool keep = t < nt && e < C && u2[t] <= T2;
       const uint64_t mk = __builtin_amdgcn_ballot_w64(keep);
       if (mk) {  // wave-uniform
         const float dv = cd[e < C ? e : 0];
@@ -2535,6 +2592,12 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
       attr_done |= 1ull << dev;
     }
   }
+#ifdef T3_MFMA  // A/B build: T3 on the matrix cores in its own launch (tolerance mode)
+  if (t3.nblk > 0 && (d / M) <= 16) {
+    hipLaunchKernelGGL(k_t3_mfma, dim3((unsigned)t3.nblk), dim3(256), 0, s, x, nq, d, cb, M, T3out);
+    t3.nblk = 0;
+  }
+#endif
   hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
                      (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
 }
@@ -2661,7 +2724,10 @@ bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 ||
 // G x R <= 8 (the per-wave top-k state).  For k > 64 at M <= 16, G = 2 and three
 // workgroups per CU beat G = 4 with two (k = 100 at C2: 174 vs 225 us, r02 A/B).
 constexpr int scan_group(int M, int R) {
-  return (M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16)) ? 4
+#ifndef SCAN_R2_G4
+#define SCAN_R2_G4 0
+#endif
+  return (M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16 && !SCAN_R2_G4)) ? 4
          : (M * 1024 * 2 <= 65536 && 2 * R <= 8)                      ? 2
                                                                       : 1;
 }

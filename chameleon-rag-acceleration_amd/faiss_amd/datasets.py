@@ -105,13 +105,18 @@ def evaluate(index, xq, gt, k):
     return (t1 - t0) * 1000.0 / nq, recalls
 
 
-def synthetic_sift_like(n, d=128, seed=1234, n_centres=10000, sigma=16.0, centre_seed=20251015):
+def synthetic_sift_like(n, d=128, seed=1234, n_centres=200_000, sigma=16.0, centre_seed=20251015):
     """Clustered, SIFT-like (non-negative integer valued) float32 vectors.
 
-    SURVEY.md §8(d): 10,000 Gaussian centres ~ U[0,128)^d shared by base, train
-    and query sets; points = clip(round(centre + N(0, sigma^2)), 0, 255).
-    Uniform random data gives poor PQ recall
-    (``Chameleon/Faiss_experiments/generate_SYN_dataset.py:4-5``).
+    SURVEY.md §8(d): Gaussian centres ~ U[0,128)^d shared by base, train and
+    query sets; points = clip(round(centre + N(0, sigma^2)), 0, 255).  Uniform
+    random data gives poor PQ recall (``Chameleon/Faiss_experiments/
+    generate_SYN_dataset.py:4-5``).  The centre count is tuned so that the
+    IVF1024,PQ16 recall-vs-nprobe curve tracks real SIFT1M's
+    (``Chameleon/Faiss_experiments/README.md:266-273``: R1@10 0.8907 at nprobe
+    16): 200,000 centres give 0.897 (10,000, the survey's first suggestion,
+    saturate at 0.455: with ~100 points per tight blob the nearest neighbour is
+    not separable by the PQ distances).  DESIGN.md §6 has both curves.
     """
     crng = np.random.default_rng(centre_seed)
     centres = crng.uniform(0.0, 128.0, size=(n_centres, d)).astype(np.float32)

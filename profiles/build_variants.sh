@@ -11,8 +11,9 @@ for spec in "$@"; do
   mkdir -p "$O"
   /opt/rocm/bin/hipcc $F -mllvm -amdgpu-atomic-optimizer-strategy=None $defs -c -o "$O/k.o" "$C/ivfpq_kernels.hip" &
   /opt/rocm/bin/hipcc $F $defs -x hip -c -o "$O/i.o" "$C/ivfpq_index.cpp" &
+  /opt/rocm/bin/hipcc $F $defs -c -o "$O/b.o" "$C/ivfpq_build.hip" &
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libivfpq.so" "$O/k.o" "$O/i.o"
-  rm -f "$O/k.o" "$O/i.o"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libivfpq.so" "$O/k.o" "$O/b.o" "$O/i.o"
+  rm -f "$O/k.o" "$O/i.o" "$O/b.o"
   echo "built $name ($defs)"
 done
