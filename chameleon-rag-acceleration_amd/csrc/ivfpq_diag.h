@@ -40,8 +40,10 @@ __device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
     if (tid == 0 && blockIdx.x < kDiagWG && it_no < kDiagItems)                               \
       g_diag[((size_t)blockIdx.x * kDiagItems + it_no) * kDiagSlots + (slot)] = (uint64_t)(v); \
   } while (0)
+#define DIAG_ONLY(...) __VA_ARGS__  // statements kept in diagnostic builds only (counters)
 #else
 #define DIAG(slot, v) \
   do {                \
   } while (0)
+#define DIAG_ONLY(...)
 #endif

@@ -1574,9 +1574,14 @@ __device__ __forceinline__ int2 fused_plan_prefix(const ListPlan& pl, int nloc, 
   return make_int2(ta, tb);
 }
 
-// word (lane & 15) of item e's record (layout of write_item)
-__device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& pl, int nloc, int G, int e, int n0,
-                                            const uint16_t* ex0, const uint16_t* ex1, const uint16_t* ord, int lane) {
+// word (lane & 15) of item e's record (layout of write_item), as RAW loads that
+// nothing here consumes (no wait: the record is in flight during the current
+// item's scan); unpack derives the fields: word 1 = the list's pair count
+// (count = min(G, min(c, cap) - t G), t in word 14), words 2 / 3 = the low
+// words of off[l + 1] / off[l] (n = w2 - w3), word 4 = off[l]'s high word.
+__device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& pl, int nloc, int e, int n0,
+                                            const uint16_t* ex0, const uint16_t* ex1, const uint16_t* ord, int G,
+                                            int lane) {
   const int kind = e < n0 ? 0 : 1;
   const int ek = kind ? e - n0 : e;
   const uint16_t* ex = kind ? ex1 : ex0;
@@ -1589,24 +1594,19 @@ __device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& p
   const int jl = ord[j];
   const int t = ek - (int)ex[j];
   const int64_t l = a.list_lo + jl;
+  const int* off32 = reinterpret_cast<const int*>(a.list_off);
+  const int* bk32 = reinterpret_cast<const int*>(pl.bucket);
   const int w = lane & 15;
   int v = 0;
-  if (w == 0) {
-    v = (int)l;
-  } else if (w == 1) {
-    v = min(G, min(pl.cnt[kind * nloc + jl], pl.cap) - t * G);
-  } else if (w == 2) {
-    v = (int)(a.list_off[l + 1] - a.list_off[l]);
-  } else if (w <= 4) {
-    const int64_t b = a.list_off[l];
-    v = w == 3 ? (int)(uint32_t)(uint64_t)b : (int)(uint32_t)((uint64_t)b >> 32);
-  } else if (w <= 12) {  // slots past the item's count hold other pairs: never used
-    const int g = (w - 5) & 3;
-    const int2 be = pl.bucket[((int64_t)jl * 2 + kind) * pl.cap + min(t * G + g, pl.cap - 1)];
-    v = w <= 8 ? be.x : be.y;
-  } else if (w == 13) {
-    v = kind;
-  }
+  if (w == 0) v = (int)l;
+  else if (w == 1) v = pl.cnt[kind * nloc + jl];
+  else if (w == 2) v = off32[2 * (l + 1)];
+  else if (w == 3) v = off32[2 * l];
+  else if (w == 4) v = off32[2 * l + 1];
+  else if (w <= 12)  // slots past the item's count hold other pairs: never used
+    v = bk32[2 * (((int64_t)jl * 2 + kind) * pl.cap + min(t * G + ((w - 5) & 3), pl.cap - 1)) + (w <= 8 ? 0 : 1)];
+  else if (w == 13) v = kind;
+  else if (w == 14) v = t;
   return v;
 }
 
@@ -1669,12 +1669,18 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   Item<G> it;
   auto fetch_rec = [&](int idx) __attribute__((always_inline)) -> int {
     if (!pl.fused) return pl.recs[(int64_t)idx * 16 + (lane & 15)];
-    return fused_record(a, pl, nloc, G, idx, n_items0, s_ex[0], s_ex[1], s_ord, lane);
+    return fused_record(a, pl, nloc, idx, n_items0, s_ex[0], s_ex[1], s_ord, G, lane);
   };
   auto unpack = [&](int rv) __attribute__((always_inline)) {
     it.l = __builtin_amdgcn_readlane(rv, 0);
-    it.cnt = __builtin_amdgcn_readlane(rv, 1);
-    it.n = __builtin_amdgcn_readlane(rv, 2);
+    if (pl.fused) {  // raw words (fused_record)
+      const int t = __builtin_amdgcn_readlane(rv, 14);
+      it.cnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - t * G);
+      it.n = __builtin_amdgcn_readlane(rv, 2) - __builtin_amdgcn_readlane(rv, 3);
+    } else {
+      it.cnt = __builtin_amdgcn_readlane(rv, 1);
+      it.n = __builtin_amdgcn_readlane(rv, 2);
+    }
     it.beg = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
                        (uint32_t)__builtin_amdgcn_readlane(rv, 3));
     it.kind = __builtin_amdgcn_readlane(rv, 13);
@@ -1790,11 +1796,13 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
     for (int g = 0; g < G; g++) tk[g].init(k);
     int qn[G];  // this wave's queue fills (wave-uniform)
+    DIAG_ONLY(uint64_t d_gather = 0, d_push = 0, d_drain = 0, d_loose = 0, d_admit = 0, d_fdrain = 0;)
 #pragma unroll
     for (int g = 0; g < G; g++) qn[g] = 0;
 
     // drain the queues into the per-query top-k lists and publish the bounds
     auto drain = [&]() __attribute__((always_inline)) {
+      DIAG_ONLY(d_drain++;)
       for (int b0 = 0; b0 < QG; b0 += 64) {
         bool any = false;
 #pragma unroll
@@ -1842,6 +1850,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     // admitted chunk by chunk.  A straight sequence of guarded blocks
     // (compile-time register indices, no selection network) stops where the
     // queue needs draining; one drain site serves every stop.
+    DIAG(11, __builtin_amdgcn_s_memtime());
     for (int sb = 0; sb < n; sb += 256 * JB) {
       if (sb > 0) {
 #pragma unroll
@@ -1852,6 +1861,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       }
       const int tn = min(JB, (n - sb + 255) >> 8);  // chunks with codes (wave-uniform)
       const bool last_sb = sb + 256 * JB >= n;
+      DIAG_ONLY(const uint64_t tg0 = __builtin_amdgcn_s_memtime();)
       // G keys per code: dis0 + sum_m LUT[m][code_m], sequential in m (the
       // oracle's order); two chunks at a time, their 2 x M LDS gathers
       // interleaved m-outer for latency hiding
@@ -1882,6 +1892,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
           }
         }
       }
+      DIAG_ONLY(asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1])); d_gather += __builtin_amdgcn_s_memtime() - tg0;)
       if constexpr (R == 1) {
         // A query without a bound gets one from this super-batch: the k-th
         // smallest of the 64 lane minima bounds the final k-th key (those minima
@@ -1933,6 +1944,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         if (g < ci.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));
         loose = loose || bound[g] == kInf;
       }
+      DIAG_ONLY(const uint64_t tb0 = __builtin_amdgcn_s_memtime(); d_loose += tb0 - tg0;)
       int t = 0;
       bool pend = false;  // a drain requested by the last chunk
       // Most super-batches of a query that already has a bound admit nothing:
@@ -1981,6 +1993,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
                     qi[wave][sl] = i;
                   }
                   qn[g] += __popcll(mk[g]);
+                  DIAG_ONLY(d_push += __popcll(mk[g]);)
                 }
                 if (loose) {  // a query of the item has no bound yet: get one now
                   stop = j + 1;
@@ -2001,13 +2014,20 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       bool queued = false;
 #pragma unroll
       for (int g = 0; g < G; g++) queued = queued || qn[g] > 0;
+      DIAG_ONLY(const uint64_t tc0 = __builtin_amdgcn_s_memtime(); d_admit += tc0 - tb0;)
       if (pend || (last_sb && queued)) {
         drain();
       }
+      DIAG_ONLY(asm volatile("" ::"v"(tk[0].p[0])); d_fdrain += __builtin_amdgcn_s_memtime() - tc0;)
     }
     DIAG(2, __builtin_amdgcn_s_memtime());
     DIAG(4, n);
     DIAG(5, ci.cnt | (ci.kind << 8));
+    DIAG(6, d_gather);
+    DIAG(7, d_push | (d_drain << 32));
+    DIAG(8, d_loose);
+    DIAG(9, d_admit);
+    DIAG(10, d_fdrain);
 
     if (nxt >= 0) {  // the next item's fields; with kEarly its first loads start here
       unpack(nrec);
@@ -2722,12 +2742,10 @@ void launch_plan_items(const ListPlan& pl, const int64_t* list_off, int lo, int 
 bool scan_supported_M(int M) { return M == 8 || M == 16 || M == 32 || M == 48 || M == 64; }
 // Pairs per work item: G LUTs of M x 256 floats interleaved in LDS (<= 64 KB),
 // G x R <= 8 (the per-wave top-k state).  For k > 64 at M <= 16, G = 2 and three
-// workgroups per CU beat G = 4 with two (k = 100 at C2: 174 vs 225 us, r02 A/B).
+// workgroups per CU beat G = 4 with two (k = 100 at C2: 174 vs 225 us, r02 A/B;
+// r03 on the 200k-centre data: 4.08 vs 3.38 M queries/s).
 constexpr int scan_group(int M, int R) {
-#ifndef SCAN_R2_G4
-#define SCAN_R2_G4 0
-#endif
-  return (M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16 && !SCAN_R2_G4)) ? 4
+  return (M * 1024 * 4 <= 65536 && 4 * R <= 8 && !(R >= 2 && M <= 16)) ? 4
          : (M * 1024 * 2 <= 65536 && 2 * R <= 8)                      ? 2
                                                                       : 1;
 }

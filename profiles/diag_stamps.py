@@ -1,12 +1,12 @@
 """Per-item phase breakdown of k_scan_lists from a DIAG_STAMPS build.
 
-Slots per (workgroup, iteration): 0 scanners start, 1 builders done (the
-next item's LUT), 2 scanners' gathers done, 3 partial writes done, 4 codes,
-5 pairs | kind << 8, 6 admitted candidates (scanner wave 0).  "build" is the
-builders' time for the NEXT item measured from this iteration's start.
+Slots per (workgroup, iteration), thread 0: 0 item start (barrier A), 1 LUT
+built (barrier B), 2 scan done, 3 partial writes done, 4 codes, 5 pairs |
+kind << 8, 6 wave 0's cycles in the super-batch gathers, 7 its admitted
+candidates | drains << 32.
 
 Usage (on the GPU box):
-  bash profiles/build_variants.sh diag:"-DDIAG_STAMPS=1"     # here, before gpurun
+  bash profiles/build_variants.sh diag:"-DDIAG_STAMPS"     # here, before gpurun
   IVFPQ_LIB=chameleon-rag-acceleration_amd/lib/var/diag/libivfpq.so python3 profiles/diag_stamps.py
 
 Builds the C2 index (bench.py's workload), runs a few warm-up searches, then one
@@ -22,7 +22,7 @@ import numpy as np
 
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(R, "chameleon-rag-acceleration_amd"))
-WG, ITEMS, SLOTS = 1024, 64, 8
+WG, ITEMS, SLOTS = 1024, 64, 16  # ivfpq_diag.h kDiagWG, kDiagItems, kDiagSlots
 
 
 def main():
@@ -62,16 +62,14 @@ def main():
         if not sel.any():
             continue
         print(f"-- {kname}: codes/item {n[sel].mean():.0f}, pairs/item {cnt[sel].mean():.2f}, "
-              f"admitted (wave 0, all g) per item {push[sel].mean():.1f}")
+              f"admitted (wave 0, all pairs) {(tau[sel] & 0xFFFFFFFF).mean():.1f}, drains {(tau[sel] >> 32).mean():.2f}, "
+              f"gather cycles (wave 0) {push[sel].mean():.0f}")
+        d_loose, d_admit, d_fdrain, t_loop = (a[:, :, i][sel] for i in (8, 9, 10, 11))
+        print(f"   scan phase (wave 0): setup {(t_loop - t1[sel]).mean():.0f}, gathers {push[sel].mean():.0f}, "
+              f"bounds {d_loose.mean():.0f}, admission {d_admit.mean():.0f}, final drain {d_fdrain.mean():.0f}")
         for name, v in (("build", (t1 - t0)[sel]), ("scan", (t2 - t1)[sel]), ("write", (t3 - t2)[sel])):
             print(f"   {name:6s} cycles mean {v.mean():8.0f} p50 {np.median(v):8.0f} p90 {np.percentile(v, 90):8.0f}")
         sc = (t2 - t1)[sel]
-        if not os.environ.get("FINE"):
-            print(f"   drain cycles (wave 0) mean {tau[sel].mean():.0f} p50 {np.median(tau[sel]):.0f}")
-        if os.environ.get("DRAINCNT"):
-            pv = push[sel]
-            print(f"   drains/item {(pv >> 48).mean():.2f}  bulk-merge cycles/item {(pv & 0xFFFFFF).mean():.0f}  "
-                  f"insert cycles/item {((pv >> 24) & 0xFFFFFF).mean():.0f}")
         print(f"   scan cycles per code-pair {sc.sum() / (n[sel] * cnt[sel]).sum():.2f}, per code {sc.sum() / n[sel].sum():.2f}")
     first = np.where(valid, t0, np.iinfo(np.int64).max).min(1)
     last = np.where(valid, t3, 0).max(1)
@@ -80,12 +78,6 @@ def main():
     busy = ((t3 - t0) * valid).sum(1)[act]
     g0 = first[act].min()
     gend = last[act].max()
-    if os.environ.get("FINE"):
-        for kname, sel in (("kind0", valid & (kind == 0)), ("kind1", valid & (kind == 1))):
-            b = (push - t1)[sel]
-            c = (tau - push)[sel]
-            d = (t2 - tau)[sel]
-            print(f"   FINE {kname}: B->bounds {b.mean():.0f}  bounds->codes ready {c.mean():.0f}  chunks+drain {d.mean():.0f}")
     print(f"WG span mean {span.mean():.0f} max {span.max():.0f} cycles; busy frac {busy.sum() / span.sum():.3f}; "
           f"kernel span {gend - g0} cycles")
     print(f"WG start offset p50 {np.median(first[act] - g0):.0f} max {(first[act] - g0).max():.0f}; "
