@@ -1512,6 +1512,16 @@ struct Item {
 // final k-th; a stale read is only a looser bound).
 constexpr int QCAP = 256;  // per-wave candidate queue entries
 
+
+// x / d for 0 <= x <= 2^24 by a float reciprocal (|error| <= 2 there) and a
+// correction from the remainder (an integer division is a ~40-instruction
+// sequence on the GPU)
+__device__ __forceinline__ int div_small(int x, int d, float inv_d) {
+  const int q = (int)((float)x * inv_d);
+  const int r = x - q * d;
+  return q + (r >= d) + (r >= 2 * d) - (r < 0) - (r < -d);
+}
+
 // ---- fused planning: the list scan derives its work items itself
 // (pl.fused: nloc <= kFusedPlanLists and fewer than 65536 items).  Every
 // workgroup forms the exclusive prefix of the per-list item counts
@@ -1632,8 +1642,13 @@ __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTo
     if (lane == 0) pl.partN[slot] = n;
 }
 
-template <int M, int G, int R, int JB>
+// ROWK (k <= 16, G = 4, R = 1): the 4 pairs' running top-k share one 64-bit
+// word per lane, pair g in the 16 lanes of row g, so one 16-lane merge network
+// (DPP row operations) serves all 4 pairs at once and one store writes their
+// partial lists.
+template <int M, int G, int R, int JB, bool ROWK = false>
 __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) {
+  static_assert(!ROWK || (G == 4 && R == 1), "row-packed top-k: 4 pairs, k <= 16");
   using V = typename LutVec<G>::T;
   constexpr int LUTN = M * 256;
   constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table
@@ -1643,6 +1658,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   __shared__ int32_t qi[4][QCAP];  // positions in the list
   __shared__ int s_next;
   __shared__ int32_t s_wb[G];  // the item's per-query bounds found by its waves (ordered ints)
+  __shared__ int s_qn[4][G];   // queue fills of the slot-counter admission
   // fused planning (pl.fused): the item prefix of every list in scheduling order
   __shared__ uint16_t s_ex[2][kFusedPlanLists + 1];
   __shared__ uint16_t s_ord[kFusedPlanLists];
@@ -1654,6 +1670,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   const int ip = a.ip;
   const int nloc = a.list_hi - a.list_lo;
   const uint64_t lanemask_lt = (1ull << lane) - 1;
+  const float inv_np = 1.0f / (float)a.nprobe;
   int n_items, n_items0 = 0;
   if (pl.fused) {
     const int2 t = fused_plan_prefix(pl, nloc, G, s_ex[0], s_ex[1], s_ord, reinterpret_cast<int*>(qi));
@@ -1689,6 +1706,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       it.pair[g] = __builtin_amdgcn_readlane(rv, 5 + g);
       it.d0[g] = __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g));
     }
+    // the pairs' queries (pair / nprobe; absent pairs: the first pair's), once per item
+#pragma unroll
+    for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
   };
 
   if (tid == 0) {
@@ -1713,7 +1733,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   CodeWords<M> cw[JB];
   float4 b1[2][U], b3[2][U][G];
   auto t3row = [&](int g) __attribute__((always_inline)) {
-    return reinterpret_cast<const float4*>(a.T3 + (int64_t)((g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe) * LUTN);
+    return reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN);
   };
   // IP has no T1: read (and ignore) a T3 row instead, so that every load is unconditional
   auto t1row = [&]() __attribute__((always_inline)) {
@@ -1733,7 +1753,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   };
   auto issue = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int g = 0; g < G; g++) tq[g] = pl.tauq[(g < it.cnt ? it.pair[g] : it.pair[0]) / a.nprobe];
+    for (int g = 0; g < G; g++) tq[g] = pl.tauq[it.q[g]];
     fetch(0, 0);
   };
   // (with R > 1 the larger top-k state leaves no registers for that: issued at the item start)
@@ -1779,40 +1799,86 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     if (tid < G) s_wb[tid] = f2ord(kInf);
     __syncthreads();  // (B) the LUT, s_next and s_wb are visible
     DIAG(1, __builtin_amdgcn_s_memtime());
-    const Item<G> ci = it;
     const int nxt = s_next;
     const int nrec = fetch_rec(nxt >= 0 ? nxt : cur);  // the next record, in flight during the scan
-    int64_t qix[G];
+    int qix[G];  // the pairs' queries
     float bound[G];
     bool loose = false;  // some query of the item has no bound yet
 #pragma unroll
     for (int g = 0; g < G; g++) {
-      qix[g] = (g < ci.cnt ? ci.pair[g] : 0) / a.nprobe;
-      bound[g] = g < ci.cnt ? ord2f(tq[g]) : -kInf;
+      qix[g] = it.q[g];
+      bound[g] = g < it.cnt ? ord2f(tq[g]) : -kInf;
       loose = loose || bound[g] == kInf;
     }
 
-    PackedTopK<R> tk[G];
+    PackedTopK<R> tk[ROWK ? 1 : G];
+    uint64_t rk = kKcNone;  // ROWK: row g = pair g's sorted top-16
+    uint64_t rtp[G];        // ROWK: pair g's k-th word (admission threshold)
 #pragma unroll
-    for (int g = 0; g < G; g++) tk[g].init(k);
+    for (int g = 0; g < G; g++) rtp[g] = kKcNone;
+    if constexpr (!ROWK)
+#pragma unroll
+      for (int g = 0; g < G; g++) tk[g].init(k);
     int qn[G];  // this wave's queue fills (wave-uniform)
     DIAG_ONLY(uint64_t d_gather = 0, d_push = 0, d_drain = 0, d_loose = 0, d_admit = 0, d_fdrain = 0;)
 #pragma unroll
     for (int g = 0; g < G; g++) qn[g] = 0;
 
     // drain the queues into the per-query top-k lists and publish the bounds
+    auto drain_rows = [&]() __attribute__((always_inline)) {
+      // lane 16 g + e takes queue entry b0 + e of pair g; 16 entries per pair per pass
+      int qmax = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
+      const int rg = lane >> 4, re = lane & 15;
+      int qr = qn[0];  // this lane's pair's fill
+#pragma unroll
+      for (int g = 1; g < G; g++) qr = rg == g ? qn[g] : qr;
+      uint64_t thr = rtp[0];
+#pragma unroll
+      for (int g = 1; g < G; g++) thr = rg == g ? rtp[g] : thr;
+      for (int b0 = 0; b0 < qmax; b0 += 16) {
+        const int e = b0 + re;
+        uint64_t c = e < qr ? pack_kc(qd[wave][rg * QG + e], qi[wave][rg * QG + e]) : kKcNone;
+        c = c < thr ? c : kKcNone;
+        if (__builtin_amdgcn_ballot_w64(c != kKcNone) == 0) continue;
+        kc_steps<2, 1>(c, lane);
+        kc_steps<4, 2>(c, lane);
+        kc_steps<8, 4>(c, lane);
+        kc_steps<128, 8>(c, lane);  // every row ascending
+        const uint64_t rv = ((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(c >> 32)) << 32) |
+                            (uint32_t)rev16_i((int)(uint32_t)c);
+        uint64_t q = rv < rk ? rv : rk;
+        kc_steps<128, 8>(q, lane);
+        rk = q;
+#pragma unroll
+        for (int g = 0; g < G; g++) rtp[g] = readlane_u64(rk, 16 * g + k - 1);
+        thr = rtp[0];
+#pragma unroll
+        for (int g = 1; g < G; g++) thr = rg == g ? rtp[g] : thr;
+      }
+#pragma unroll
+      for (int g = 0; g < G; g++) bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
+    };
     auto drain = [&]() __attribute__((always_inline)) {
       DIAG_ONLY(d_drain++;)
-      for (int b0 = 0; b0 < QG; b0 += 64) {
+      if constexpr (ROWK) drain_rows();
+      else for (int b0 = 0; b0 < QG; b0 += 64) {
         bool any = false;
 #pragma unroll
         for (int g = 0; g < G; g++) any = any || b0 < qn[g];
         if (!any) break;
+        // every pair's queued words first (one LDS round trip for all of them)
+        uint64_t cwg[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          const int e = b0 + lane;
+          cwg[g] = e < qn[g] ? pack_kc(qd[wave][g * QG + e], qi[wave][g * QG + e]) : kKcNone;
+        }
 #pragma unroll
         for (int g = 0; g < G; g++) {
           if (b0 >= qn[g]) continue;
-          const int e = b0 + lane;
-          const uint64_t cw64 = e < qn[g] ? pack_kc(qd[wave][g * QG + e], qi[wave][g * QG + e]) : kKcNone;
+          const uint64_t cw64 = cwg[g];
           const bool p = cw64 < tk[g].tp;
           const uint64_t mk = __ballot(p);
           if (!mk) continue;
@@ -1838,9 +1904,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
       for (int g = 0; g < G; g++) {
         loose = loose || bound[g] == kInf;
-        if (g < ci.cnt && tk[g].tp != kKcNone && lane == 0) {
-          atomicMin(&s_wb[g], f2ord(tk[g].td()));
-          atomicMin(&pl.tauq[qix[g]], f2ord(tk[g].td()));
+        const uint64_t tp = ROWK ? rtp[g] : tk[ROWK ? 0 : g].tp;
+        if (g < it.cnt && tp != kKcNone && lane == 0) {
+          atomicMin(&s_wb[g], f2ord(kc_key(tp)));
+          atomicMin(&pl.tauq[qix[g]], f2ord(kc_key(tp)));
         }
       }
     };
@@ -1880,7 +1947,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
           for (int h = 0; h < 2; h++)
 #pragma unroll
-            for (int g = 0; g < G; g++) dis[2 * jd + h][g] = ci.d0[g];
+            for (int g = 0; g < G; g++) dis[2 * jd + h][g] = it.d0[g];
 #pragma unroll
           for (int m = 0; m < M; m++) {
 #pragma unroll
@@ -1941,25 +2008,64 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       loose = false;
 #pragma unroll
       for (int g = 0; g < G; g++) {
-        if (g < ci.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));
+        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));
         loose = loose || bound[g] == kInf;
       }
       DIAG_ONLY(const uint64_t tb0 = __builtin_amdgcn_s_memtime(); d_loose += tb0 - tg0;)
       int t = 0;
       bool pend = false;  // a drain requested by the last chunk
-      // Most super-batches of a query that already has a bound admit nothing:
-      // one compare per (chunk, pair) and a single ballot decide that, and the
-      // per-chunk admission below runs only when some lane passes.
-      bool anyc = false;
+      // One bit per (chunk, pair) and lane: code of chunk j passes pair g's bound.
+      // Most super-batches of a query that already has a bound admit nothing (one
+      // ballot decides that); when every queue has room for all of them, the
+      // candidates take queue slots from per-wave LDS counters (one atomic per
+      // candidate, no per-(chunk, pair) ballots); otherwise, and while a query
+      // has no bound yet, the per-chunk admission below runs.
+      uint32_t bits = 0;
 #pragma unroll
       for (int j = 0; j < JB; j++) {
         if (j < tn) {  // wave-uniform
           const bool valid = sb + j * 256 + wave * 64 + lane < n;
 #pragma unroll
-          for (int g = 0; g < G; g++) anyc = anyc || (valid && dis[j][g] <= bound[g]);
+          for (int g = 0; g < G; g++) bits |= (uint32_t)(valid && dis[j][g] <= bound[g]) << (j * G + g);
         }
       }
-      if (__builtin_amdgcn_ballot_w64(anyc) == 0) t = tn;  // nothing to admit in this super-batch
+      if (__builtin_amdgcn_ballot_w64(bits != 0) == 0) {
+        t = tn;  // nothing to admit in this super-batch
+      } else if (!loose) {
+        const int c = __popc(bits);  // this lane's candidates (<= JB x G < 32)
+        int tot = 0;
+#pragma unroll
+        for (int b = 0; b < 5; b++) tot += __popcll(__builtin_amdgcn_ballot_w64((c >> b) & 1)) << b;
+        int qmax = 0;
+#pragma unroll
+        for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
+        if (qmax + tot <= QG) {
+          if (lane == 0)
+#pragma unroll
+            for (int g = 0; g < G; g++) s_qn[wave][g] = qn[g];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int j = 0; j < JB; j++) {
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              if ((bits >> (j * G + g)) & 1u) {
+                const int sl = g * QG + atomicAdd(&s_qn[wave][g], 1);
+                qd[wave][sl] = dis[j][g];
+                qi[wave][sl] = sb + j * 256 + wave * 64 + lane;
+              }
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int g = 0; g < G; g++) qn[g] = s_qn[wave][g];
+          DIAG_ONLY(d_push += tot;)
+          t = tn;
+        }
+      }
       while (t < tn) {
         int stop = tn;       // first chunk not yet admitted
         bool want = false;   // drain requested
@@ -2018,26 +2124,39 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       if (pend || (last_sb && queued)) {
         drain();
       }
-      DIAG_ONLY(asm volatile("" ::"v"(tk[0].p[0])); d_fdrain += __builtin_amdgcn_s_memtime() - tc0;)
+      DIAG_ONLY(asm volatile("" ::"v"(ROWK ? rk : tk[0].p[0])); d_fdrain += __builtin_amdgcn_s_memtime() - tc0;)
     }
     DIAG(2, __builtin_amdgcn_s_memtime());
     DIAG(4, n);
-    DIAG(5, ci.cnt | (ci.kind << 8));
+    DIAG(5, it.cnt | (it.kind << 8));
     DIAG(6, d_gather);
     DIAG(7, d_push | (d_drain << 32));
     DIAG(8, d_loose);
     DIAG(9, d_admit);
     DIAG(10, d_fdrain);
 
+    // each wave writes its own sorted partial list per pair (merged by k_merge_probes)
+    if constexpr (ROWK) {  // lane 16 g + e: entry e of pair g, one store for all pairs
+      const int rg = lane >> 4, re = lane & 15;
+      int pr = it.pair[0];
+#pragma unroll
+      for (int g = 1; g < G; g++) pr = rg == g ? it.pair[g] : pr;
+      if (rg < it.cnt && re < k) {
+        const int64_t o = ((int64_t)pr * 4 + wave) * k + re;
+        const bool empty = rk == kKcNone;
+        pl.partD[o] = empty ? FLT_MAX : kc_key(rk);
+        pl.partI[o] = empty ? -1 : it.beg + (int64_t)(uint32_t)rk;
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (g >= it.cnt) continue;
+        write_partial<R>(pl, tk[g], (int64_t)it.pair[g] * 4 + wave, k, it.beg, lane);
+      }
+    }
     if (nxt >= 0) {  // the next item's fields; with kEarly its first loads start here
       unpack(nrec);
       if constexpr (kEarly) issue();
-    }
-    // each wave writes its own sorted partial list per pair (merged by k_merge_probes)
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      if (g >= ci.cnt) continue;
-      write_partial<R>(pl, tk[g], (int64_t)ci.pair[g] * 4 + wave, k, ci.beg, lane);
     }
     DIAG(3, __builtin_amdgcn_s_memtime());
     it_no++;
@@ -2786,7 +2905,15 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   // 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
   constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : 2;
   if (ev) (void)hipEventRecord(ev[0], s);
-  hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+  if constexpr (G == 4 && R == 1) {
+    if (a.k <= 16) {  // r03 A/B at C2: 115.1 vs 125.7 us
+      hipLaunchKernelGGL((k_scan_lists<M, G, R, JB, true>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+    } else {
+      hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+    }
+  } else {
+    hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+  }
   if (ev) (void)hipEventRecord(ev[1], s);
   if (R >= 2 && a.nprobe <= 64) hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
