@@ -312,3 +312,30 @@ def test_c4_shape_eight_list_range_shards(c4_shape, k):
     del shards, parts
     Dr, Ir = ox.search(xq, k)
     assert_same(torch.cat(Dm).cpu().numpy(), torch.cat(Im).cpu().numpy(), Dr, Ir)
+
+
+def test_precomputed_tables_on_a_side_stream(sift1m):
+    """bench.py's shard step computes T3 of the global batch on a side stream
+    (precompute_tables_device) while the coarse step runs; the preassigned search
+    of exactly those queries then uses it.  Results equal the plain preassigned
+    search and the oracle, over several back-to-back steps (the next step's T3
+    is ordered after the previous search that read the buffer)."""
+    import torch
+
+    ix, ox, xq = sift1m
+    ix.nprobe = ox.nprobe = 16
+    xd = torch.from_numpy(xq).cuda()
+    Dq, Iq = ix.coarse_device(xd)
+    Dr, Ir = ox.search(xq, 10)
+    side = torch.cuda.Stream()
+    for step in range(3):
+        side.wait_stream(torch.cuda.current_stream())
+        ix.precompute_tables_device(xd, stream=side.cuda_stream)
+        D, I = ix.search_preassigned_device(xd, 10, Iq, Dq)
+        torch.cuda.synchronize()
+        assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+    # tables of another batch are not used for this one
+    ix.precompute_tables_device(xd[:512].contiguous(), stream=side.cuda_stream)
+    D, I = ix.search_preassigned_device(xd, 10, Iq, Dq)
+    torch.cuda.synchronize()
+    assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
