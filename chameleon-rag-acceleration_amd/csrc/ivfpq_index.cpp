@@ -176,9 +176,8 @@ struct ivfpq_index {
   bool dirty = true;
   hipStream_t stream = nullptr;
   // scratch
-  DevBuf w_x, w_xn, w_dist, w_lists, w_dis0, w_T3, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
+  DevBuf w_x, w_xn, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
   DevBuf h_D, h_I, h_Iq, h_Dq;  // device staging of the host-buffer entry points
-  DevBuf w_cand;                // segment candidates of the large-nlist coarse quantizer
   // device-side add: the new entries of one add call, and the image merge scratch
   DevBuf a_lists, a_ids, a_codes, a_scratch, a_off;
   bool host_stale = false;  // the device image holds entries the host lists lack (device-side adds)
@@ -188,66 +187,104 @@ struct ivfpq_index {
   const float* pre_x = nullptr;
   int64_t pre_n = 0;
   hipEvent_t pre_ev = nullptr;
-  // list-major plan workspaces (ivfpq_kernels.h ListPlan)
-  DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
-  // Stream ordering of the per-handle workspaces: every device search records
-  // `done` on its stream; the next search (on any stream) waits for it, and
-  // anything that frees or rewrites device buffers synchronizes on it first.
-  hipEvent_t done = nullptr;
-  hipStream_t done_stream = nullptr;
-  bool done_pending = false;
+  // The per-batch workspaces of a device search (coarse keys, probes, T3, the
+  // list-major plan of ivfpq_kernels.h ListPlan and the partial lists).  A handle
+  // holds kSlots of them, one per stream in use (begin_slot), so that up to
+  // kSlots batches can be in flight on different streams at once: the next
+  // batch's coarse step and list scan start while this batch's scan drains
+  // (DESIGN.md §4).
+  struct Work {
+    DevBuf w_dist, w_lists, w_dis0, w_T3, w_cand;  // w_cand: large-nlist coarse segment candidates
+    DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
+    // every use records `done` on its stream; the slot's next user (on another
+    // stream) waits for it, and whatever frees or rewrites shared device buffers
+    // synchronizes on every slot's first
+    hipEvent_t done = nullptr;
+    hipStream_t done_stream = nullptr;
+    bool done_pending = false;
+    uint64_t last_use = 0;
+  };
+  static constexpr int kSlots = 3;
+  Work work[kSlots];
+  int slot = 0;  // the workspace of the current (last begun) device call
+  uint64_t uses = 0;
   std::mutex mu;
 
-  void order_after_last(hipStream_t s) {
-    if (done_pending && done_stream != s) HIPCHECK(hipStreamWaitEvent(s, done, 0));
+  Work& W() { return work[slot]; }
+  // The workspace of a device call on stream s: the one last used on s (stream
+  // order already protects it, and a one-stream caller keeps a single
+  // workspace), else the least recently used one, ordered after its last user.
+  void begin_slot(hipStream_t s) {
+    int pick = -1;
+    for (int i = 0; i < kSlots && pick < 0; i++)
+      if (work[i].done_pending && work[i].done_stream == s) pick = i;
+    if (pick < 0) {
+      pick = 0;
+      for (int i = 1; i < kSlots; i++)
+        if (work[i].last_use < work[pick].last_use) pick = i;
+    }
+    slot = pick;
+    Work& w = work[slot];
+    w.last_use = ++uses;
+    if (w.done_pending && w.done_stream != s) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
+  }
+  // ordered after every device call still in flight (for paths that touch the
+  // shared staging buffers or T3-ahead state)
+  void order_after_all(hipStream_t s) {
+    for (auto& w : work)
+      if (w.done_pending && w.done_stream != s) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
   }
   void mark_done(hipStream_t s) {
-    HIPCHECK(hipEventRecord(done, s));
-    done_stream = s;
-    done_pending = true;
+    Work& w = W();
+    HIPCHECK(hipEventRecord(w.done, s));
+    w.done_stream = s;
+    w.done_pending = true;
   }
   void quiesce() {
-    if (done_pending) HIPCHECK(hipEventSynchronize(done));
-    done_pending = false;
+    for (auto& w : work) {
+      if (w.done_pending) HIPCHECK(hipEventSynchronize(w.done));
+      w.done_pending = false;
+    }
   }
 
   ListPlan make_plan(int64_t nq, int np, int k, hipStream_t s) {
     const int nloc = std::max(list_hi - list_lo, 1);
+    Work& w = W();
     const int G = list_scan_group(M, k);
     ListPlan pl;
     pl.cap = (int)nq;
     pl.max_items = list_scan_max_items(nq * np, nloc, G);
     pl.grid = scan_lists_grid(M, k);
-    if (!p_cnt.p || p_cnt.bytes < sizeof(int32_t) * 2 * nloc) {
+    if (!w.p_cnt.p || w.p_cnt.bytes < sizeof(int32_t) * 2 * nloc) {
       // kept zero between batches by k_scan_lists; zeroed once here
-      p_cnt.ensure(sizeof(int32_t) * 2 * nloc);
-      HIPCHECK(hipMemsetAsync(p_cnt.p, 0, p_cnt.bytes, s));
+      w.p_cnt.ensure(sizeof(int32_t) * 2 * nloc);
+      HIPCHECK(hipMemsetAsync(w.p_cnt.p, 0, w.p_cnt.bytes, s));
     }
-    p_bucket.ensure(sizeof(int2) * 2 * (size_t)nloc * nq);
-    p_recs.ensure(sizeof(int32_t) * 16 * (size_t)pl.max_items);
-    if (!p_hdr.p) {  // hdr[2] (the scan's work counter) is kept zero between batches by k_merge_probes
-      p_hdr.ensure(sizeof(int32_t) * 16);
-      HIPCHECK(hipMemsetAsync(p_hdr.p, 0, p_hdr.bytes, s));
+    w.p_bucket.ensure(sizeof(int2) * 2 * (size_t)nloc * nq);
+    w.p_recs.ensure(sizeof(int32_t) * 16 * (size_t)pl.max_items);
+    if (!w.p_hdr.p) {  // hdr[2] (the scan's work counter) is kept zero between batches by k_merge_probes
+      w.p_hdr.ensure(sizeof(int32_t) * 16);
+      HIPCHECK(hipMemsetAsync(w.p_hdr.p, 0, w.p_hdr.bytes, s));
     }
-    p_D.ensure(sizeof(float) * nq * np * 4 * k);
-    p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
-    p_N.ensure(sizeof(int32_t) * nq * np * 4);
-    if (!p_done.p || p_done.bytes < sizeof(int32_t) * nq) {  // kept zero between batches by k_merge_probes
-      p_done.ensure(sizeof(int32_t) * nq);
-      HIPCHECK(hipMemsetAsync(p_done.p, 0, p_done.bytes, s));
+    w.p_D.ensure(sizeof(float) * nq * np * 4 * k);
+    w.p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
+    w.p_N.ensure(sizeof(int32_t) * nq * np * 4);
+    if (!w.p_done.p || w.p_done.bytes < sizeof(int32_t) * nq) {  // kept zero between batches by k_merge_probes
+      w.p_done.ensure(sizeof(int32_t) * nq);
+      HIPCHECK(hipMemsetAsync(w.p_done.p, 0, w.p_done.bytes, s));
     }
-    p_tau.ensure(sizeof(int32_t) * nq);
-    p_qmask.ensure(sizeof(uint64_t) * nq);
-    pl.cnt = p_cnt.as<int32_t>();
-    pl.bucket = p_bucket.as<int2>();
-    pl.recs = p_recs.as<int32_t>();
-    pl.hdr = p_hdr.as<int32_t>();
-    pl.partD = p_D.as<float>();
-    pl.partI = p_I.as<int64_t>();
-    pl.partN = p_N.as<int32_t>();
-    pl.qdone = p_done.as<int32_t>();
-    pl.tauq = p_tau.as<int32_t>();
-    pl.qmask = p_qmask.as<uint64_t>();
+    w.p_tau.ensure(sizeof(int32_t) * nq);
+    w.p_qmask.ensure(sizeof(uint64_t) * nq);
+    pl.cnt = w.p_cnt.as<int32_t>();
+    pl.bucket = w.p_bucket.as<int2>();
+    pl.recs = w.p_recs.as<int32_t>();
+    pl.hdr = w.p_hdr.as<int32_t>();
+    pl.partD = w.p_D.as<float>();
+    pl.partI = w.p_I.as<int64_t>();
+    pl.partN = w.p_N.as<int32_t>();
+    pl.qdone = w.p_done.as<int32_t>();
+    pl.tauq = w.p_tau.as<int32_t>();
+    pl.qmask = w.p_qmask.as<uint64_t>();
     pl.order = d_order.p ? d_order.as<int32_t>() : nullptr;
     pl.fused = scan_fused_plan(nloc, pl.max_items, M) ? 1 : 0;
     return pl;
@@ -308,14 +345,16 @@ struct ivfpq_index {
       (void)hipEventDestroy(m.b);
     }
     for (auto e : ev_pool) (void)hipEventDestroy(e);
-    if (done) (void)hipEventDestroy(done);
+    for (auto& w : work)
+      if (w.done) (void)hipEventDestroy(w.done);
     if (pre_ev) (void)hipEventDestroy(pre_ev);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
   void init_stream() {
     if (!stream) HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    if (!done) HIPCHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    for (auto& w : work)
+      if (!w.done) HIPCHECK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
     if (!pre_ev) HIPCHECK(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
   }
 
@@ -327,7 +366,7 @@ struct ivfpq_index {
                    int64_t* assign_host, const float* x_dev = nullptr, bool ip_assign = false) {
     const int64_t rows = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nc * 4)));
     w_xn.ensure(sizeof(float) * rows);
-    w_dist.ensure(sizeof(float) * rows * nc);
+    W().w_dist.ensure(sizeof(float) * rows * nc);
     w_D.ensure(sizeof(float) * rows);
     w_I.ensure(sizeof(int64_t) * rows);
     if (!x_dev) w_x.ensure(sizeof(float) * rows * dd);
@@ -341,8 +380,8 @@ struct ivfpq_index {
         xd = w_x.as<float>();
       }
       if (!ip_assign) launch_row_norms(xd, c, dd, w_xn.as<float>(), stream);
-      launch_l2_dist(xd, w_xn.as<float>(), c, dc, dcn, nc, dd, w_dist.as<float>(), stream, ip_assign);
-      launch_select_rows(w_dist.as<float>(), c, nc, 1, w_D.as<float>(), w_I.as<int64_t>(), stream);
+      launch_l2_dist(xd, w_xn.as<float>(), c, dc, dcn, nc, dd, W().w_dist.as<float>(), stream, ip_assign);
+      launch_select_rows(W().w_dist.as<float>(), c, nc, 1, w_D.as<float>(), w_I.as<int64_t>(), stream);
       HIPCHECK(hipGetLastError());
       HIPCHECK(hipMemcpyAsync(assign_host + r0, w_I.p, sizeof(int64_t) * c, hipMemcpyDeviceToHost, stream));
       HIPCHECK(hipStreamSynchronize(stream));
@@ -469,7 +508,7 @@ struct ivfpq_index {
     require(trained, "index is not trained");
     if (n <= 0) return;
     upload_lists();  // host-side adds not yet in the image
-    order_after_last(s);
+    order_after_all(s);
     quiesce();
     const int64_t rows = nlist >= kSegmentedNlist ? std::min<int64_t>(n, 1 << 18)
                                                   : std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
@@ -590,21 +629,21 @@ struct ivfpq_index {
   bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
                      const ListPlan* plan = nullptr, float* T3out = nullptr) {
     if (nlist >= kSegmentedNlist && np <= 64) {  // large nlist: no [c][nlist] key matrix
-      w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist) * np);
+      W().w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist) * np);
       if (T3out) launch_ip_table(x, c, d, d_cb.as<float>(), M, ksub, T3out, s);
-      launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, w_cand.as<uint64_t>(), dis,
-                              lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
+      launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, W().w_cand.as<uint64_t>(),
+                              dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
       return plan != nullptr;
     }
-    w_dist.ensure(sizeof(float) * c * nlist);
-    launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, w_dist.as<float>(), s, ip(), T3out,
+    W().w_dist.ensure(sizeof(float) * c * nlist);
+    launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, W().w_dist.as<float>(), s, ip(), T3out,
                        d_cb.as<float>(), M);
     if (np <= 64) {
-      launch_coarse_select(w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
+      launch_coarse_select(W().w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
                            list_hi, x, d_cent.as<float>(), d);
       return plan != nullptr;
     }
-    launch_select_rows(w_dist.as<float>(), c, nlist, np, dis, lists, s, ip());
+    launch_select_rows(W().w_dist.as<float>(), c, nlist, np, dis, lists, s, ip());
     return false;
   }
 
@@ -614,7 +653,7 @@ struct ivfpq_index {
     check_search(n, k);
     upload_lists();
     if (n == 0) return;
-    order_after_last(s);
+    begin_slot(s);
     const int np = preassigned ? nprobe : eff_nprobe();
     const int nloc = std::max(list_hi - list_lo, 1);
     // queries per chunk: [c][nlist] keys, T3 and buckets within kChunkBytes; the
@@ -624,10 +663,10 @@ struct ivfpq_index {
     const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)nloc * 16});
     const int64_t qc = std::max<int64_t>(
         1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * k * 48))}));
-    w_T3.ensure(sizeof(float) * qc * M * ksub);
+    W().w_T3.ensure(sizeof(float) * qc * M * ksub);
     if (!preassigned) {
-      w_lists.ensure(sizeof(int64_t) * qc * np);
-      w_dis0.ensure(sizeof(float) * qc * np);
+      W().w_lists.ensure(sizeof(int64_t) * qc * np);
+      W().w_dis0.ensure(sizeof(float) * qc * np);
     }
     const int G = list_scan_group(M, k);
     const bool use_pre = preassigned && pre_x == x && pre_n == n;
@@ -644,20 +683,21 @@ struct ivfpq_index {
         launch_plan_count(lists, (Dq && !ip()) ? Dq + q0 * np : nullptr, xq, d_cent.as<float>(), c, d, np,
                           d_off.as<int64_t>(), list_lo, list_hi, ip(), true, k, plan, s);
       } else {
-        planned = coarse_launch(xq, c, np, w_dis0.as<float>(), w_lists.as<int64_t>(), s, &plan, w_T3.as<float>());
-        lists = w_lists.as<int64_t>();
+        planned =
+            coarse_launch(xq, c, np, W().w_dis0.as<float>(), W().w_lists.as<int64_t>(), s, &plan, W().w_T3.as<float>());
+        lists = W().w_lists.as<int64_t>();
         if (!planned)
-          launch_plan_count(lists, ip() ? nullptr : w_dis0.as<float>(), xq, d_cent.as<float>(), c, d, np,
+          launch_plan_count(lists, ip() ? nullptr : W().w_dis0.as<float>(), xq, d_cent.as<float>(), c, d, np,
                             d_off.as<int64_t>(), list_lo, list_hi, ip(), false, k, plan, s);
       }
       mark_end(tm, s);
-      const float* T3 = w_T3.as<float>();
+      const float* T3 = W().w_T3.as<float>();
       if (preassigned && use_pre) {  // T3 computed ahead on another stream
         HIPCHECK(hipStreamWaitEvent(s, pre_ev, 0));
         T3 = w_T3pre.as<float>() + q0 * M * ksub;
       } else if (preassigned) {  // T3 (the coarse launch builds it otherwise)
         const int tt = mark_begin(ST_TABLES, s);
-        launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, w_T3.as<float>(), s);
+        launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, W().w_T3.as<float>(), s);
         mark_end(tt, s);
       }
       ScanArgs a;
@@ -694,7 +734,7 @@ struct ivfpq_index {
   void tables_dev(int64_t n, const float* x, hipStream_t s) {
     require(trained, "index is not trained");
     if (n <= 0) return;
-    order_after_last(s);
+    order_after_all(s);
     w_T3pre.ensure(sizeof(float) * (size_t)n * M * ksub);
     launch_ip_table(x, n, d, d_cb.as<float>(), M, ksub, w_T3pre.as<float>(), s);
     HIPCHECK(hipGetLastError());
@@ -706,7 +746,7 @@ struct ivfpq_index {
   void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {
     require(trained, "index is not trained");
     if (n <= 0) return;
-    order_after_last(s);
+    begin_slot(s);
     const int np = eff_nprobe();
     const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
@@ -723,7 +763,7 @@ struct ivfpq_index {
                    bool preassigned) {
     check_search(n, k);
     if (n == 0) return;
-    order_after_last(stream);
+    order_after_all(stream);
     const int np = nprobe;
     w_x.ensure(sizeof(float) * n * d);
     h_D.ensure(sizeof(float) * n * k);
@@ -783,7 +823,7 @@ struct ivfpq_index {
     require(ans != nullptr && cap >= need, "answer buffer holds " + std::to_string(cap) + " bytes, the answer needs " +
                                                std::to_string(need));
     check_search(B, (int)k);
-    order_after_last(stream);
+    order_after_all(stream);
     w_x.ensure(qbytes);
     h_D.ensure(sizeof(float) * B * k);
     h_I.ensure(sizeof(int64_t) * B * k);

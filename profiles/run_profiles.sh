@@ -23,6 +23,7 @@ python3 $R/profiles/make_pmc_json.py "$OUT/pmc" "$KEY" "$OUT/scan_pmc.json" "$LI
 timeout -k 10 400 python3 $R/bench.py --pmc-json "$OUT/scan_pmc.json" "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 $R/bench.py --pmc-json "$OUT/scan_pmc.json" "$@" > "$OUT/bench_traced.json" 2> "$OUT/bench_traced.err" || exit $?
-python3 $R/profiles/summarize_trace.py "$OUT/trace/run_kernel_trace.csv" 20 > "$OUT/kernel_summary.txt" 2>&1
-cat "$OUT/bench.json"; head -14 "$OUT/kernel_summary.txt"
+WK=$(python3 -c "import json; j=json.loads(open('$OUT/bench_traced.json').read().strip().splitlines()[-1]); print(j['warmup'], j['steps'])")
+python3 $R/profiles/summarize_trace.py "$OUT/trace/run_kernel_trace.csv" 20 --passes $WK > "$OUT/kernel_summary.txt" 2>&1
+cat "$OUT/bench.json"; head -24 "$OUT/kernel_summary.txt"
 echo "profiles done: $OUT"
