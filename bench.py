@@ -180,6 +180,10 @@ def main():
         else:  # stream j of the in-flight set, with its own output buffers
             ix.search_device(xq_dev[b], k, Dbufs[j], Ibufs[j], stream=streams[j].cuda_stream)
 
+    if not shard:  # setup: each in-flight stream's workspace allocated (one search each), whatever --warmup is
+        for j in range(inflight):
+            step(j % args.nbatches, j)
+        torch.cuda.synchronize()
     for w in range(args.warmup):
         step(w % args.nbatches, w % inflight)
     torch.cuda.synchronize()

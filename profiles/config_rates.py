@@ -3,6 +3,7 @@
 points, queries resident in HBM), next to bench.py's C2 line:
 
   C1  SIFT1M-shaped IVF1024,PQ16, nprobe 8, k 10 (bench.py's index, other nprobe)
+  C2  bench.py's index (200k centres), nprobe 16, k 10 and k 100
   C3  BEIR-NQ-shaped: d 768, nb 2.68 M, IVF4096,PQ64, nprobe 32, METRIC_INNER_PRODUCT,
       k 10 and k 1000 (beir EvaluateRetrieval's top_k, evaluation.py:13)
   C4  Deep1B-shaped single-GPU shard at reduced size: d 96, nb --c4-nb, IVF65536,PQ48,
@@ -12,7 +13,8 @@ Synthetic clustered data (faiss_amd.datasets.synthetic_sift_like; for C3 centred
 normalised to unit rows like sentence embeddings), GPU-trained with
 few iterations (rates do not depend on training quality).  Prints one JSON line per
 (config, k): queries/s and ms per 1024-query batch, from torch events on the
-launch stream over --reps batches.
+launch stream over --reps batches, and the same with two batches in flight on two
+streams (wall clock).
 """
 import argparse
 import json
@@ -42,7 +44,21 @@ def rate(ix, xq_dev, k, reps):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    return {"k": k, "ms_per_batch": ms, "queries_per_s": B / (ms * 1e-3)}
+    # the same batches two in flight (batch r on stream r % 2, own outputs; wall clock
+    # between device-wide synchronisations), as bench.py's timed region
+    ss = [torch.cuda.Stream() for _ in range(2)]
+    outs = [(D, I), (torch.empty_like(D), torch.empty_like(I))]
+    for r in range(4):  # warm: each stream's workspace allocated before timing
+        ix.search_device(xq_dev[(r % nb) * B:(r % nb + 1) * B], k, *outs[r % 2], stream=ss[r % 2].cuda_stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in range(reps):
+        b = r % nb
+        ix.search_device(xq_dev[b * B:(b + 1) * B], k, *outs[r % 2], stream=ss[r % 2].cuda_stream)
+    torch.cuda.synchronize()
+    ms2 = (time.perf_counter() - t0) * 1000.0 / reps
+    return {"k": k, "ms_per_batch": ms, "queries_per_s": B / (ms * 1e-3),
+            "ms_per_batch_inflight2": ms2, "queries_per_s_inflight2": B / (ms2 * 1e-3)}
 
 
 def embed_like(x, mu):
@@ -93,6 +109,16 @@ def main():
         r = rate(ix, xq, 10, a.reps)
         print(json.dumps({"config": "C1 shape on GPU: SIFT1M-shaped IVF1024,PQ16 nprobe 8", **r,
                           "setup_s": time.time() - t0}), flush=True)
+        del ix, xq
+    if "c2" in only:
+        t0 = time.time()
+        ix, _ = build(faiss, datasets, 128, 1024, 16, 1_000_000, 100_000, 25, faiss.METRIC_L2, 200_000)
+        xq = torch.from_numpy(datasets.synthetic_sift_like(10240, 128, seed=123)).cuda()
+        ix.nprobe = 16
+        for k in (10, 100):
+            r = rate(ix, xq, k, a.reps)
+            print(json.dumps({"config": "C2: SIFT1M-shaped IVF1024,PQ16 nprobe 16 (bench.py's index)", **r,
+                              "setup_s": time.time() - t0}), flush=True)
         del ix, xq
     if "c3" in only:
         t0 = time.time()
