@@ -91,7 +91,7 @@ def parse():
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
     p.add_argument("--inflight", type=int, default=2,
                    help="batches in flight on that many HIP streams (step s on stream s %% N): the next batch's "
-                        "coarse step overlaps this batch's list scan; 1 = serial (shard mode is always serial)")
+                        "coarse step overlaps this batch's list scan; 1 = serial")
     return p.parse_args()
 
 
@@ -148,7 +148,7 @@ def main():
 
     xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
     k = args.k
-    inflight = 1 if shard else max(1, args.inflight)
+    inflight = max(1, args.inflight)
     streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
     Dbufs = [torch.empty((Bg, k), dtype=torch.float32, device=dev) for _ in range(inflight)]
     Ibufs = [torch.empty((Bg, k), dtype=torch.int64, device=dev) for _ in range(inflight)]
@@ -165,25 +165,26 @@ def main():
     bytes_lists = bytes_alg
 
     merged = {}
-    side = torch.cuda.Stream(dev) if shard else None
+    sides = [torch.cuda.Stream(dev) for _ in range(inflight)] if shard else None
 
     def step(b, j=0):
         if shard:  # coarse for this rank's slice, probes all-gathered, own lists scanned for the batch
             xg = xq_dev[b]
-            # T3 of the global batch on a side stream, concurrent with the coarse step and the all_gather
-            ix.precompute_tables_device(xg, stream=side.cuda_stream)
-            Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
-            Dq, Iq = all_gather_probes(Dq_s, Iq_s, world)
-            Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbuf, Ibuf)
-            Ds, Is = exchange_partials(Dp, Ip, world)
-            merged[b] = faiss.merge_topk_device(Ds, Is)
+            with torch.cuda.stream(streams[j]):  # collectives and kernels of this batch on stream j
+                # T3 of the global batch on a side stream, concurrent with the coarse step and the all_gather
+                sides[j].wait_stream(streams[j])
+                ix.precompute_tables_device(xg, stream=sides[j].cuda_stream)
+                Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
+                Dq, Iq = all_gather_probes(Dq_s, Iq_s, world)
+                Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j])
+                Ds, Is = exchange_partials(Dp, Ip, world)
+                merged[b] = faiss.merge_topk_device(Ds, Is)
         else:  # stream j of the in-flight set, with its own output buffers
             ix.search_device(xq_dev[b], k, Dbufs[j], Ibufs[j], stream=streams[j].cuda_stream)
 
-    if not shard:  # setup: each in-flight stream's workspace allocated (one search each), whatever --warmup is
-        for j in range(inflight):
-            step(j % args.nbatches, j)
-        torch.cuda.synchronize()
+    for j in range(inflight):  # setup: each in-flight stream's workspace allocated, whatever --warmup is
+        step(j % args.nbatches, j)
+    torch.cuda.synchronize()
     for w in range(args.warmup):
         step(w % args.nbatches, w % inflight)
     torch.cuda.synchronize()

@@ -183,10 +183,20 @@ struct ivfpq_index {
   bool host_stale = false;  // the device image holds entries the host lists lack (device-side adds)
   // T3 of a batch computed ahead (ivfpq_precompute_tables_device), consumed by the
   // next preassigned search of exactly those queries
-  DevBuf w_T3pre;
-  const float* pre_x = nullptr;
-  int64_t pre_n = 0;
-  hipEvent_t pre_ev = nullptr;
+  struct PreT3 {
+    DevBuf buf;
+    const float* x = nullptr;  // tag: the queries (pointer, n) it was computed for; null = free
+    int64_t n = 0;
+    uint64_t seq = 0;
+    hipEvent_t ready = nullptr;  // recorded after the table launch
+    hipStream_t ready_stream = nullptr;
+    hipEvent_t freed = nullptr;  // recorded after the consuming search's scans
+    hipStream_t freed_stream = nullptr;
+    bool ready_pending = false, freed_pending = false;
+  };
+  static constexpr int kPreT3 = 3;  // tables of up to three batches ahead (batches in flight)
+  PreT3 pre[kPreT3];
+  uint64_t pre_seq = 0;
   // The per-batch workspaces of a device search (coarse keys, probes, T3, the
   // list-major plan of ivfpq_kernels.h ListPlan and the partial lists).  A handle
   // holds kSlots of them, one per stream in use (begin_slot), so that up to
@@ -347,7 +357,10 @@ struct ivfpq_index {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     for (auto& w : work)
       if (w.done) (void)hipEventDestroy(w.done);
-    if (pre_ev) (void)hipEventDestroy(pre_ev);
+    for (auto& p : pre) {
+      if (p.ready) (void)hipEventDestroy(p.ready);
+      if (p.freed) (void)hipEventDestroy(p.freed);
+    }
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -355,7 +368,10 @@ struct ivfpq_index {
     if (!stream) HIPCHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     for (auto& w : work)
       if (!w.done) HIPCHECK(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
-    if (!pre_ev) HIPCHECK(hipEventCreateWithFlags(&pre_ev, hipEventDisableTiming));
+    for (auto& p : pre) {
+      if (!p.ready) HIPCHECK(hipEventCreateWithFlags(&p.ready, hipEventDisableTiming));
+      if (!p.freed) HIPCHECK(hipEventCreateWithFlags(&p.freed, hipEventDisableTiming));
+    }
   }
 
   // ---------------------------------------------------------------- helpers
@@ -669,8 +685,16 @@ struct ivfpq_index {
       W().w_dis0.ensure(sizeof(float) * qc * np);
     }
     const int G = list_scan_group(M, k);
-    const bool use_pre = preassigned && pre_x == x && pre_n == n;
-    pre_x = nullptr;  // consumed (or stale)
+    // tables computed ahead (tables_dev) are consumed in order: the oldest entry for
+    // exactly these queries; entries computed before it, or all of them when none
+    // matches, are stale and dropped
+    int pi = -1;
+    if (preassigned)
+      for (int i = 0; i < kPreT3; i++)
+        if (pre[i].x == x && pre[i].n == n && (pi < 0 || pre[i].seq < pre[pi].seq)) pi = i;
+    for (auto& p : pre)
+      if (p.x && (pi < 0 || p.seq <= pre[pi].seq)) p.x = nullptr;
+    const bool use_pre = pi >= 0;
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
       const float* xq = x + q0 * d;
@@ -693,8 +717,8 @@ struct ivfpq_index {
       mark_end(tm, s);
       const float* T3 = W().w_T3.as<float>();
       if (preassigned && use_pre) {  // T3 computed ahead on another stream
-        HIPCHECK(hipStreamWaitEvent(s, pre_ev, 0));
-        T3 = w_T3pre.as<float>() + q0 * M * ksub;
+        if (pre[pi].ready_stream != s) HIPCHECK(hipStreamWaitEvent(s, pre[pi].ready, 0));
+        T3 = pre[pi].buf.as<float>() + q0 * M * ksub;
       } else if (preassigned) {  // T3 (the coarse launch builds it otherwise)
         const int tt = mark_begin(ST_TABLES, s);
         launch_ip_table(xq, c, d, d_cb.as<float>(), M, ksub, W().w_T3.as<float>(), s);
@@ -724,23 +748,40 @@ struct ivfpq_index {
       mark_end(ts, s);
       HIPCHECK(hipGetLastError());
     }
+    if (use_pre) {  // the entry's buffer may be rewritten once these scans are done
+      HIPCHECK(hipEventRecord(pre[pi].freed, s));
+      pre[pi].freed_stream = s;
+      pre[pi].freed_pending = true;
+    }
     mark_done(s);
   }
 
   // T3 [n][M][ksub] of the queries x, on stream s, ahead of a preassigned search
   // of exactly those queries (the shard flow computes it while the probes are
-  // all-gathered); ordered after the handle's previous search, which may still read
-  // the buffer.
+  // all-gathered), into one of kPreT3 buffers so that batches in flight each have
+  // their own.
   void tables_dev(int64_t n, const float* x, hipStream_t s) {
     require(trained, "index is not trained");
     if (n <= 0) return;
-    order_after_all(s);
-    w_T3pre.ensure(sizeof(float) * (size_t)n * M * ksub);
-    launch_ip_table(x, n, d, d_cb.as<float>(), M, ksub, w_T3pre.as<float>(), s);
+    // the free entry computed longest ago, else the oldest pending one (dropped);
+    // ordered after its last consumer's scans and its last table launch
+    int r = 0;
+    for (int i = 1; i < kPreT3; i++) {
+      const bool fi = pre[i].x == nullptr, fr = pre[r].x == nullptr;
+      if ((fi && !fr) || (fi == fr && pre[i].seq < pre[r].seq)) r = i;
+    }
+    PreT3& p = pre[r];
+    if (p.freed_pending && p.freed_stream != s) HIPCHECK(hipStreamWaitEvent(s, p.freed, 0));
+    if (p.ready_pending && p.ready_stream != s) HIPCHECK(hipStreamWaitEvent(s, p.ready, 0));
+    p.buf.ensure(sizeof(float) * (size_t)n * M * ksub);
+    launch_ip_table(x, n, d, d_cb.as<float>(), M, ksub, p.buf.as<float>(), s);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipEventRecord(pre_ev, s));
-    pre_x = x;
-    pre_n = n;
+    HIPCHECK(hipEventRecord(p.ready, s));
+    p.ready_stream = s;
+    p.ready_pending = true;
+    p.x = x;
+    p.n = n;
+    p.seq = ++pre_seq;
   }
 
   void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {

@@ -113,8 +113,10 @@ int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int
  * ahead of a search_preassigned_device of exactly those queries (same pointer
  * and n), which then uses them instead of building its own.  The shard flow
  * issues it on a side stream while the coarse step and the probe all-gather run
- * (T3 depends only on the queries).  The next search on the handle consumes the
- * tables; it must be for the same queries (pointer, n and contents unchanged).
+ * (T3 depends only on the queries).  Tables are consumed in order: a search takes
+ * the oldest pending tables of its queries (pointer, n and contents unchanged
+ * since the call) and drops older ones; a search matching none drops all.  Up to
+ * three can be pending, so a shard loop can keep batches in flight.
  * Reference: IndexIVFPQ::search_preassigned's
  * per-query precompute_list_tables (bench_gpu_1bn.py:605-616 shard step). */
 int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream);

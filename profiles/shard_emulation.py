@@ -10,6 +10,9 @@ global batch of 1024 x N queries.
                the batch), scan
   merge    : merge_topk_device of the rank's slice over N partials
 
+  step_wall_ms: the whole per-rank step by wall clock, one batch at a time and with two
+               batches in flight on two streams (as bench.py runs it)
+
 Collectives are not run (one GPU): their per-rank bytes are printed instead
 (all_gather of the probes: N x 1024 x nprobe x 12 B; all_to_all of partials:
 N x 1024 x k x 12 B).  Usage: python3 profiles/shard_emulation.py [--nb 1000000]
@@ -18,6 +21,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -79,6 +83,32 @@ def main():
                 t["coarse"] += e[0].elapsed_time(e[1]) / args.reps
                 t["preassigned"] += e[1].elapsed_time(e[2]) / args.reps
                 t["merge"] += e[2].elapsed_time(e[3]) / args.reps
+        # the whole per-rank step (T3 ahead on a side stream, coarse of the own slice,
+        # preassigned search, merge), wall clock over reps steps: one stream, then
+        # two batches in flight (step s on compute stream s % 2 with its own side stream)
+        comp = [torch.cuda.Stream() for _ in range(2)]
+        sides = [torch.cuda.Stream() for _ in range(2)]
+        outs = [(torch.empty((N * B, k), device="cuda"), torch.empty((N * B, k), dtype=torch.int64, device="cuda"))
+                for _ in range(2)]
+
+        def rank_step(j):
+            with torch.cuda.stream(comp[j]):
+                sides[j].wait_stream(comp[j])
+                sh.precompute_tables_device(xg, stream=sides[j].cuda_stream)
+                sh.coarse_device(xg[:B])
+                Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j])
+                faiss.merge_topk_device(torch.stack([Dp[:B]] * N), torch.stack([Ip[:B]] * N))
+
+        wall = {}
+        for label, depth in (("serial", 1), ("inflight2", 2)):
+            for s in range(4):
+                rank_step(s % depth)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for s in range(args.reps * 5):
+                rank_step(s % depth)
+            torch.cuda.synchronize()
+            wall[label] = (time.perf_counter() - t0) * 1000.0 / (args.reps * 5)
         sh.set_timing(True)
         for _ in range(args.reps):
             sh.search_preassigned_device(xg, k, Iq_all, Dq_all)
@@ -86,7 +116,8 @@ def main():
         sh.set_timing(False)
         st = sh.get_timing()
         split = {s: v[0] / max(v[1], 1) for s, v in st.items()}
-        row = {"N": N, "lists": [lo, hi], "batch": N * B, "ms": t, "preassigned_stages_ms": split,
+        row = {"N": N, "lists": [lo, hi], "batch": N * B, "ms": t, "step_wall_ms": wall,
+               "preassigned_stages_ms": split,
                "allgather_bytes_per_rank": N * B * npb * 12, "alltoall_bytes_per_rank": N * B * k * 12}
         print(json.dumps(row), flush=True)
         out.append(row)

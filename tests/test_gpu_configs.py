@@ -339,3 +339,39 @@ def test_precomputed_tables_on_a_side_stream(sift1m):
     D, I = ix.search_preassigned_device(xd, 10, Iq, Dq)
     torch.cuda.synchronize()
     assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+
+
+def test_precomputed_tables_with_batches_in_flight(sift1m):
+    """The shard step pipelined: 8 batches (4 distinct query sets, so tables of
+    the same pointer recur) issued on 2 compute streams, each with its own side
+    stream for the T3 ahead, and with the T3 of batch s + 1 issued before the
+    search of batch s (tables consumed in order), with no synchronisation.
+    Every batch equals its plain preassigned search."""
+    import torch
+
+    ix, ox, xq = sift1m
+    ix.nprobe = 16
+    B = 256
+    xs = [torch.from_numpy(xq[i * B:(i + 1) * B]).cuda() for i in range(4)]
+    ref = []
+    for x in xs:
+        Dq, Iq = ix.coarse_device(x)
+        D, I = ix.search_preassigned_device(x, 10, Iq, Dq)
+        torch.cuda.synchronize()
+        ref.append((D.cpu().numpy(), I.cpu().numpy()))
+    comp = [torch.cuda.Stream() for _ in range(2)]
+    side = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    outs = []
+    ix.precompute_tables_device(xs[0], stream=side[0].cuda_stream)
+    for s in range(8):
+        j = s % 2
+        x = xs[s % 4]
+        if s + 1 < 8:  # the next batch's tables first
+            ix.precompute_tables_device(xs[(s + 1) % 4], stream=side[(s + 1) % 2].cuda_stream)
+        with torch.cuda.stream(comp[j]):
+            Dq, Iq = ix.coarse_device(x)
+            outs.append(ix.search_preassigned_device(x, 10, Iq, Dq))
+    torch.cuda.synchronize()
+    for s, (D, I) in enumerate(outs):
+        assert_same(D.cpu().numpy(), I.cpu().numpy(), *ref[s % 4])
