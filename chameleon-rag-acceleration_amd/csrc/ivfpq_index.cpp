@@ -236,7 +236,15 @@ struct ivfpq_index {
     slot = pick;
     Work& w = work[slot];
     w.last_use = ++uses;
-    if (w.done_pending && w.done_stream != s) HIPCHECK(hipStreamWaitEvent(s, w.done, 0));
+    // Taking over another stream's workspace (more streams than kSlots) waits on
+    // the host: a device-side wait here let a k = 100 batch on a fourth stream see
+    // its predecessor's partial lists (1 batch in 480, tests/test_gpu_parity.py
+    // test_batches_in_flight_on_round_robin_streams), which two or three streams
+    // never do.
+    if (w.done_pending && w.done_stream != s) {
+      HIPCHECK(hipEventSynchronize(w.done));
+      w.done_pending = false;
+    }
   }
   // ordered after every device call still in flight (for paths that touch the
   // shared staging buffers or T3-ahead state)
