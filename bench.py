@@ -89,9 +89,10 @@ def parse():
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
-    p.add_argument("--inflight", type=int, default=2,
-                   help="batches in flight on that many HIP streams (step s on stream s %% N): the next batch's "
-                        "coarse step overlaps this batch's list scan; 1 = serial")
+    p.add_argument("--inflight", type=int, default=1,
+                   help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 sets "
+                        "IVFPQ_INFLIGHT=1 so the library lets them overlap -- experimental, DESIGN.md section 4: "
+                        "a rare k=100 mismatch was seen with overlapping batches); 1 = one stream")
     return p.parse_args()
 
 
@@ -109,6 +110,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    if args.inflight > 1:  # read by the library when it is loaded
+        os.environ["IVFPQ_INFLIGHT"] = "1"
     import faiss_amd as faiss
     from faiss_amd import datasets
     from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials

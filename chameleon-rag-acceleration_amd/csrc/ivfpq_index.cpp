@@ -158,6 +158,14 @@ constexpr size_t kPartialBytes = size_t(2048) << 20;  // bound for a chunk's per
 // C2, nlist 1024: segmented 22.5 + 8.5 us + a separate T3 launch 13.0 us vs key
 // matrix 17.8 + 10.0 us with T3 in the same launch)
 constexpr int kSegmentedNlist = 8192;
+// Batches on different streams run concurrently only with IVFPQ_INFLIGHT=1:
+// two concurrent searches showed a rare wrong k = 100 result (about 1 batch in
+// 480), so by default a search is ordered after every search
+// still in flight on another stream.
+const bool g_inflight = [] {
+  const char* e = std::getenv("IVFPQ_INFLIGHT");
+  return e && e[0] == '1';
+}();
 
 }  // namespace
 
@@ -245,6 +253,7 @@ struct ivfpq_index {
       HIPCHECK(hipEventSynchronize(w.done));
       w.done_pending = false;
     }
+    if (!g_inflight) order_after_all(s);
   }
   // ordered after every device call still in flight (for paths that touch the
   // shared staging buffers or T3-ahead state)

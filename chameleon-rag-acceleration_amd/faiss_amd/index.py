@@ -472,11 +472,11 @@ class IndexIVFPQ:
         """Search with inputs resident in HBM.  ``x`` is a torch float32 CUDA
         tensor [n, d] on the index's device; returns torch (D, I) there, launched
         on ``stream`` (default: torch's current stream).  Searches of one index
-        may be issued on different streams without synchronizing: the handle
-        keeps a per-batch workspace for each of up to three streams, so batches
-        on different streams run concurrently (the next batch's coarse step and
-        scan start while this batch's scan drains); a fourth stream waits for
-        the least recently used workspace's last search."""
+        may be issued on different streams without synchronizing: the library
+        orders each search after those still in flight on other streams.  With
+        IVFPQ_INFLIGHT=1 in the environment (experimental) the handle's
+        per-stream workspaces (up to three) let batches on different streams
+        overlap instead."""
         import torch
 
         self._check_k(k)

@@ -252,9 +252,9 @@ def test_device_searches_on_two_streams_without_sync(golden_dir):
 
 
 def test_batches_in_flight_on_round_robin_streams():
-    """Pipelined serving: 12 batches issued round robin on 4 streams with no
-    synchronisation (more streams than the handle's 3 workspaces, so workspaces
-    are reused across streams), at k = 10 (row-packed scan) and k = 100 (k > 64
+    """12 batches issued round robin on 4 streams with no synchronisation (more
+    streams than the handle's 3 workspaces, so workspaces are reused across
+    streams; the library orders the searches across streams), at k = 10 (row-packed scan) and k = 100 (k > 64
     merge), with a coarse_device + preassigned search interleaved.  Every batch
     equals its serial search on one stream, bit for bit; the serial results are
     themselves checked against the oracle for the first batch."""
