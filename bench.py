@@ -90,9 +90,9 @@ def parse():
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
     p.add_argument("--inflight", type=int, default=1,
-                   help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 sets "
-                        "IVFPQ_INFLIGHT=1 so the library lets them overlap -- experimental, DESIGN.md section 4: "
-                        "a rare k=100 mismatch was seen with overlapping batches); 1 = one stream")
+                   help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 turns the "
+                        "index's batches-in-flight mode on so that consecutive batches overlap, DESIGN.md "
+                        "section 4); 1 = one stream")
     return p.parse_args()
 
 
@@ -110,8 +110,6 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    if args.inflight > 1:  # read by the library when it is loaded
-        os.environ["IVFPQ_INFLIGHT"] = "1"
     import faiss_amd as faiss
     from faiss_amd import datasets
     from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials
@@ -152,6 +150,7 @@ def main():
     xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
     k = args.k
     inflight = max(1, args.inflight)
+    ix.inflight = inflight > 1
     streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
     Dbufs = [torch.empty((Bg, k), dtype=torch.float32, device=dev) for _ in range(inflight)]
     Ibufs = [torch.empty((Bg, k), dtype=torch.int64, device=dev) for _ in range(inflight)]
@@ -176,10 +175,10 @@ def main():
             with torch.cuda.stream(streams[j]):  # collectives and kernels of this batch on stream j
                 # T3 of the global batch on a side stream, concurrent with the coarse step and the all_gather
                 sides[j].wait_stream(streams[j])
-                ix.precompute_tables_device(xg, stream=sides[j].cuda_stream)
+                tok = ix.precompute_tables_device(xg, stream=sides[j].cuda_stream)
                 Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
                 Dq, Iq = all_gather_probes(Dq_s, Iq_s, world)
-                Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j])
+                Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j], tables=tok)
                 Ds, Is = exchange_partials(Dp, Ip, world)
                 merged[b] = faiss.merge_topk_device(Ds, Is)
         else:  # stream j of the in-flight set, with its own output buffers

@@ -158,14 +158,14 @@ constexpr size_t kPartialBytes = size_t(2048) << 20;  // bound for a chunk's per
 // C2, nlist 1024: segmented 22.5 + 8.5 us + a separate T3 launch 13.0 us vs key
 // matrix 17.8 + 10.0 us with T3 in the same launch)
 constexpr int kSegmentedNlist = 8192;
-// Batches on different streams run concurrently only with IVFPQ_INFLIGHT=1:
-// two concurrent searches showed a rare wrong k = 100 result (about 1 batch in
-// 480), so by default a search is ordered after every search
-// still in flight on another stream.
-const bool g_inflight = [] {
+// Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
+// on, device searches on different streams overlap, each on its own per-stream
+// workspace; off, a search is ordered after every search still in flight on
+// another stream.  IVFPQ_INFLIGHT=1 in the environment turns it on for new handles.
+bool inflight_default() {
   const char* e = std::getenv("IVFPQ_INFLIGHT");
   return e && e[0] == '1';
-}();
+}
 
 }  // namespace
 
@@ -189,13 +189,12 @@ struct ivfpq_index {
   // device-side add: the new entries of one add call, and the image merge scratch
   DevBuf a_lists, a_ids, a_codes, a_scratch, a_off;
   bool host_stale = false;  // the device image holds entries the host lists lack (device-side adds)
-  // T3 of a batch computed ahead (ivfpq_precompute_tables_device), consumed by the
-  // next preassigned search of exactly those queries
+  // T3 of a batch computed ahead (ivfpq_precompute_tables_device), handed to a
+  // preassigned search by the token that call returned (seq)
   struct PreT3 {
     DevBuf buf;
-    const float* x = nullptr;  // tag: the queries (pointer, n) it was computed for; null = free
     int64_t n = 0;
-    uint64_t seq = 0;
+    uint64_t seq = 0;  // the token; 0 = free
     hipEvent_t ready = nullptr;  // recorded after the table launch
     hipStream_t ready_stream = nullptr;
     hipEvent_t freed = nullptr;  // recorded after the consuming search's scans
@@ -214,6 +213,7 @@ struct ivfpq_index {
   struct Work {
     DevBuf w_dist, w_lists, w_dis0, w_T3, w_cand;  // w_cand: large-nlist coarse segment candidates
     DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
+    uint32_t epoch = 0;  // tag of the last batch planned in this workspace (ListPlan::tauq)
     // every use records `done` on its stream; the slot's next user (on another
     // stream) waits for it, and whatever frees or rewrites shared device buffers
     // synchronizes on every slot's first
@@ -226,6 +226,7 @@ struct ivfpq_index {
   Work work[kSlots];
   int slot = 0;  // the workspace of the current (last begun) device call
   uint64_t uses = 0;
+  bool inflight = inflight_default();
   std::mutex mu;
 
   Work& W() { return work[slot]; }
@@ -253,7 +254,7 @@ struct ivfpq_index {
       HIPCHECK(hipEventSynchronize(w.done));
       w.done_pending = false;
     }
-    if (!g_inflight) order_after_all(s);
+    if (!inflight) order_after_all(s);
   }
   // ordered after every device call still in flight (for paths that touch the
   // shared staging buffers or T3-ahead state)
@@ -300,7 +301,15 @@ struct ivfpq_index {
       w.p_done.ensure(sizeof(int32_t) * nq);
       HIPCHECK(hipMemsetAsync(w.p_done.p, 0, w.p_done.bytes, s));
     }
-    w.p_tau.ensure(sizeof(int32_t) * nq);
+    if (!w.p_tau.p || w.p_tau.bytes < sizeof(uint64_t) * nq) {  // all-ones: no batch's bound (ListPlan::tauq)
+      w.p_tau.ensure(sizeof(uint64_t) * nq);
+      HIPCHECK(hipMemsetAsync(w.p_tau.p, 0xff, w.p_tau.bytes, s));
+    }
+    if (++w.epoch >= 0xFFFFFFF0u) {  // tag space used up (after ~4e9 batches): start over on a clean buffer
+      if (w.done_pending) HIPCHECK(hipEventSynchronize(w.done));
+      HIPCHECK(hipMemsetAsync(w.p_tau.p, 0xff, w.p_tau.bytes, s));
+      w.epoch = 1;
+    }
     w.p_qmask.ensure(sizeof(uint64_t) * nq);
     pl.cnt = w.p_cnt.as<int32_t>();
     pl.bucket = w.p_bucket.as<int2>();
@@ -310,7 +319,9 @@ struct ivfpq_index {
     pl.partI = w.p_I.as<int64_t>();
     pl.partN = w.p_N.as<int32_t>();
     pl.qdone = w.p_done.as<int32_t>();
-    pl.tauq = w.p_tau.as<int32_t>();
+    pl.tauq = w.p_tau.as<uint64_t>();
+    pl.epoch = w.epoch;
+    pl.err = w.p_hdr.as<int32_t>() + 15;
     pl.qmask = w.p_qmask.as<uint64_t>();
     pl.order = d_order.p ? d_order.as<int32_t>() : nullptr;
     pl.fused = scan_fused_plan(nloc, pl.max_items, M) ? 1 : 0;
@@ -450,6 +461,7 @@ struct ivfpq_index {
 
   void upload_trained() {
     quiesce();
+    drop_tables();
     d_cent.ensure(sizeof(float) * nlist * d);
     d_cnorm.ensure(sizeof(float) * nlist);
     d_cb.ensure(sizeof(float) * M * ksub * (d / M));
@@ -681,36 +693,34 @@ struct ivfpq_index {
   }
 
   // The full search on device pointers, on stream s.  Iq/Dq non-null = preassigned.
+  // tables: a token of tables_dev (preassigned searches only; 0 = build T3 here)
   void search_dev(int64_t n, const float* x, int k, float* D, int64_t* I, const int64_t* Iq, const float* Dq,
-                  bool preassigned, hipStream_t s) {
+                  bool preassigned, hipStream_t s, uint64_t tables = 0) {
     check_search(n, k);
     upload_lists();
     if (n == 0) return;
     begin_slot(s);
     const int np = preassigned ? nprobe : eff_nprobe();
-    const int nloc = std::max(list_hi - list_lo, 1);
-    // queries per chunk: [c][nlist] keys, T3 and buckets within kChunkBytes; the
-    // per-wave partial lists ([c][np][4][k] keys + positions, 48 B per entry and
-    // query) within kPartialBytes, so large k still runs whole 1024-query batches
-    // (C3, k = 1000, nprobe 32: 1.5 MB per query)
-    const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)nloc * 16});
-    const int64_t qc = std::max<int64_t>(
-        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * k * 48))}));
+    const int64_t qc = query_chunk(n, np, k);
     W().w_T3.ensure(sizeof(float) * qc * M * ksub);
     if (!preassigned) {
       W().w_lists.ensure(sizeof(int64_t) * qc * np);
       W().w_dis0.ensure(sizeof(float) * qc * np);
     }
     const int G = list_scan_group(M, k);
-    // tables computed ahead (tables_dev) are consumed in order: the oldest entry for
-    // exactly these queries; entries computed before it, or all of them when none
-    // matches, are stale and dropped
+    // tables computed ahead (tables_dev): exactly the entry of the token, which
+    // this search consumes
     int pi = -1;
-    if (preassigned)
+    if (tables) {
+      require(preassigned, "precomputed tables are for preassigned searches");
       for (int i = 0; i < kPreT3; i++)
-        if (pre[i].x == x && pre[i].n == n && (pi < 0 || pre[i].seq < pre[pi].seq)) pi = i;
-    for (auto& p : pre)
-      if (p.x && (pi < 0 || p.seq <= pre[pi].seq)) p.x = nullptr;
+        if (pre[i].seq == tables) pi = i;
+      require(pi >= 0, "tables token " + std::to_string(tables) +
+                           " is not pending (already consumed, or overwritten by later precomputes)");
+      require(pre[pi].n == n, "tables token was computed for " + std::to_string(pre[pi].n) + " queries, not " +
+                                  std::to_string(n));
+      pre[pi].seq = 0;
+    }
     const bool use_pre = pi >= 0;
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
@@ -747,6 +757,7 @@ struct ivfpq_index {
       a.codes = d_codes.as<uint8_t>();
       a.ids = d_ids.as<int64_t>();
       a.list_off = d_off.as<int64_t>();
+      a.n_codes = ntotal;
       a.probe_list = lists;
       a.nq = c;
       a.nprobe = np;
@@ -773,18 +784,32 @@ struct ivfpq_index {
     mark_done(s);
   }
 
+  // The query chunk of a search: [c][nlist] keys, T3 and buckets within
+  // kChunkBytes; the per-wave partial lists ([c][np][4][k] keys + positions, 48 B
+  // per entry and query) within kPartialBytes, so large k still runs whole
+  // 1024-query batches (C3, k = 1000, nprobe 32: 1.5 MB per query).
+  int64_t query_chunk(int64_t n, int np, int k) const {
+    const int nloc = std::max(list_hi - list_lo, 1);
+    const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)nloc * 16});
+    return std::max<int64_t>(
+        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * k * 48))}));
+  }
+
   // T3 [n][M][ksub] of the queries x, on stream s, ahead of a preassigned search
   // of exactly those queries (the shard flow computes it while the probes are
   // all-gathered), into one of kPreT3 buffers so that batches in flight each have
-  // their own.
-  void tables_dev(int64_t n, const float* x, hipStream_t s) {
+  // their own.  Returns the token the search takes (ivfpq.h).
+  uint64_t tables_dev(int64_t n, const float* x, hipStream_t s) {
     require(trained, "index is not trained");
-    if (n <= 0) return;
+    require(n >= 1, "precompute_tables needs at least one query");
+    const int64_t cap = (int64_t)(kChunkBytes / ((size_t)M * ksub * 4));
+    require(n <= cap, "precompute_tables: n = " + std::to_string(n) + " exceeds the " + std::to_string(cap) +
+                          " queries one table buffer holds (split the batch)");
     // the free entry computed longest ago, else the oldest pending one (dropped);
     // ordered after its last consumer's scans and its last table launch
     int r = 0;
     for (int i = 1; i < kPreT3; i++) {
-      const bool fi = pre[i].x == nullptr, fr = pre[r].x == nullptr;
+      const bool fi = pre[i].seq == 0, fr = pre[r].seq == 0;
       if ((fi && !fr) || (fi == fr && pre[i].seq < pre[r].seq)) r = i;
     }
     PreT3& p = pre[r];
@@ -796,9 +821,13 @@ struct ivfpq_index {
     HIPCHECK(hipEventRecord(p.ready, s));
     p.ready_stream = s;
     p.ready_pending = true;
-    p.x = x;
     p.n = n;
     p.seq = ++pre_seq;
+    return p.seq;
+  }
+  // tables computed ahead are meaningless once the codebook changes or the index is reset
+  void drop_tables() {
+    for (auto& p : pre) p.seq = 0;
   }
 
   void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {
@@ -1079,6 +1108,7 @@ int ivfpq_reset(ivfpq_index* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     for (auto& v : h->lcodes) v.clear();
     for (auto& v : h->lids) v.clear();
+    h->drop_tables();
     h->host_stale = false;
     h->ntotal = 0;
     h->next_id = 0;
@@ -1161,13 +1191,55 @@ int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int
   });
 }
 
-int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream) {
+int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream, uint64_t* token) {
   return guarded([&] {
     check_handle(h);
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
-    require(n >= 0 && (n == 0 || x != nullptr), "null x");
-    h->tables_dev(n, x, stream ? (hipStream_t)stream : h->stream);
+    require(x != nullptr && token != nullptr, "null x or token");
+    *token = h->tables_dev(n, x, stream ? (hipStream_t)stream : h->stream);
+  });
+}
+
+int ivfpq_search_preassigned_tables_device(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq,
+                                           const float* Dq, float* D, int64_t* I, uint64_t token, void* stream) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(token != 0, "tables token 0 (use ivfpq_search_preassigned_device without tables)");
+    h->search_dev(n, x, k, D, I, Iq, Dq, true, (hipStream_t)stream, token);
+  });
+}
+
+int ivfpq_set_inflight(ivfpq_index* h, int on) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(on == 0 || on == 1, "inflight must be 0 or 1");
+    h->quiesce();  // searches issued under the previous setting complete first
+    h->inflight = on == 1;
+  });
+}
+
+int ivfpq_get_inflight(const ivfpq_index* h) { return h ? (h->inflight ? 1 : 0) : -1; }
+
+int ivfpq_get_error_count(ivfpq_index* h, int64_t* out) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(out != nullptr, "null output");
+    h->quiesce();
+    int64_t tot = 0;
+    for (auto& w : h->work) {
+      if (!w.p_hdr.p) continue;
+      int32_t hdr[16];
+      HIPCHECK(hipMemcpy(hdr, w.p_hdr.p, sizeof(hdr), hipMemcpyDeviceToHost));
+      tot += hdr[15];
+    }
+    *out = tot;
   });
 }
 

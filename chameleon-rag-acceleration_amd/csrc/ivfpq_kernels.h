@@ -91,7 +91,14 @@ struct ListPlan {
   int64_t* partI;    // same shape: global code positions (-1 = none; k <= 64 pads every list to k)
   int32_t* partN;    // [nq][nprobe][4] valid entries of each partial list (k > 64 writes only those)
   int32_t* qdone;    // [nq] k > 64: 1 = merged by k_merge_big (k_merge_probes resets it to 0)
-  int32_t* tauq;     // [nq] running k-th key per query (order-preserving int of the float, atomicMin)
+  // [nq] running k-th key per query, tagged with the batch: (~epoch) << 32 |
+  // order-preserving key bits, lowered by 64-bit atomicMin.  A newer batch's
+  // words compare below every older batch's, so no reset store is needed and a
+  // word left by an earlier batch reads as "no bound" (tau_get); the buffer is
+  // initialised to all-ones.  Read with agent-scope atomic loads.
+  uint64_t* tauq;
+  uint32_t epoch;    // this batch's tag (>= 1, strictly increasing per workspace)
+  int32_t* err;      // [1] index-check violations counted by the merge kernels (0 = none; never reset)
   uint64_t* qmask;   // [nq] probes the scan covers (nprobe <= 64): bit p = pair (q, p) is scanned
   int grid;          // persistent list-scan workgroups (multiple of 8)
   const int32_t* order = nullptr;  // [nloc] item order of the lists within a kind (nullable = list order)
@@ -104,6 +111,7 @@ struct ScanArgs {
   const uint8_t* codes;     // [n_codes][M], lists concatenated, each list sorted by label
   const int64_t* ids;       // [n_codes]
   const int64_t* list_off;  // [nlist + 1]
+  int64_t n_codes;          // entries in codes / ids (bound of every code position the merges dereference)
   const int64_t* probe_list;  // [nq][nprobe] (-1 = skipped probe)
   int64_t nq;
   int nprobe;

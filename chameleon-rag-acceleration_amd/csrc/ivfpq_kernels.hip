@@ -550,6 +550,27 @@ __device__ __forceinline__ void plan_pair(const ListPlan& pl, int nloc, int64_t 
   if (s < pl.cap) pl.bucket[((int64_t)(l - lo) * 2 + kind) * pl.cap + s] = make_int2(pair, __float_as_int(dis0));
 }
 
+// The query bound tau_q of this batch (an order-preserving int; "no bound" =
+// f2ord(inf) when the word still carries an earlier batch's tag).  Agent-scope
+// atomic load: other workgroups lower the word while this one runs, so the read
+// must not be served from a non-coherent cached copy.
+__device__ __forceinline__ int tau_get(const ListPlan& pl, int64_t q) {
+  const uint64_t v = __hip_atomic_load(pl.tauq + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint32_t)(v >> 32) == ~pl.epoch ? (int)((uint32_t)v ^ 0x80000000u) : f2ord(kInf);
+}
+// tau_q := min(tau_q, o) within this batch (any k real candidates bound the final k-th key)
+__device__ __forceinline__ void tau_lower(const ListPlan& pl, int64_t q, int o) {
+  const uint64_t w = ((uint64_t)(~pl.epoch) << 32) | ((uint32_t)o ^ 0x80000000u);
+  atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);
+}
+// a code position read back from a partial list, checked against the image
+// (counted in pl.err and dropped when outside it: never dereferenced)
+__device__ __forceinline__ bool pos_ok(const ScanArgs& a, const ListPlan& pl, int64_t pos) {
+  const bool bad = pos >= a.n_codes;
+  if (bad) atomicAdd(pl.err, 1);
+  return pos >= 0 && !bad;
+}
+
 // List-major planning request for the coarse selection's epilogue.
 struct CoarsePlan {
   ListPlan pl;
@@ -911,10 +932,7 @@ __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, i
     const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
     const uint64_t um = __ballot(use);
     const int fp = um ? (int)__builtin_ctzll(um) : 64;
-    if (lane == 0) {
-      cp.pl.tauq[q] = f2ord(kInf);
-      cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
-    }
+    if (lane == 0) cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
     if (use) {
       float d0 = rd;
       if (ip) {
@@ -1113,7 +1131,6 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
-  if (lane == 0) pl.tauq[q] = f2ord(kInf);
   bool found = false;
   for (int p0 = 0; p0 < nprobe; p0 += 64) {
     const int p = p0 + lane;
@@ -1707,6 +1724,18 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       it.d0[g] = __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g));
     }
     // the pairs' queries (pair / nprobe; absent pairs: the first pair's), once per item
+    // a pair id outside the batch would address another batch's tables and
+    // partial lists: counted in pl.err, and the item scans nothing
+    bool bad = false;
+#pragma unroll
+    for (int g = 0; g < G; g++)
+      bad = bad || (g < it.cnt && (unsigned)it.pair[g] >= (unsigned)(a.nq * a.nprobe));
+    if (bad) {
+      if (lane == 0) atomicAdd(pl.err, 1);
+      it.cnt = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) it.pair[g] = 0;
+    }
 #pragma unroll
     for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
   };
@@ -1753,7 +1782,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   };
   auto issue = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int g = 0; g < G; g++) tq[g] = pl.tauq[it.q[g]];
+    for (int g = 0; g < G; g++) tq[g] = tau_get(pl, it.q[g]);
     fetch(0, 0);
   };
   // (with R > 1 the larger top-k state leaves no registers for that: issued at the item start)
@@ -1907,7 +1936,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         const uint64_t tp = ROWK ? rtp[g] : tk[ROWK ? 0 : g].tp;
         if (g < it.cnt && tp != kKcNone && lane == 0) {
           atomicMin(&s_wb[g], f2ord(kc_key(tp)));
-          atomicMin(&pl.tauq[qix[g]], f2ord(kc_key(tp)));
+          tau_lower(pl, qix[g], f2ord(kc_key(tp)));
         }
       }
     };
@@ -1977,7 +2006,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
             const float T = wave_kth_smallest(mn, k, lane);
             if (T < kInf && lane == 0) {
               atomicMin(&s_wb[g], f2ord(T));
-              atomicMin(&pl.tauq[qix[g]], f2ord(T));
+              tau_lower(pl, qix[g], f2ord(T));
             }
           }
         }
@@ -2000,7 +2029,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
             const int T = (int)(wave_kth_u32<JB>(u, k) ^ 0x80000000u);  // f2ord of the k-th key
             if (lane == 0) {
               atomicMin(&s_wb[g], T);
-              atomicMin(&pl.tauq[qix[g]], T);
+              tau_lower(pl, qix[g], T);
             }
           }
         }
@@ -2311,7 +2340,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     }
     bool ok[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) ok[u] = scanned && u < k && pos[u] >= 0;
+    for (int u = 0; u < U; u++) ok[u] = scanned && u < k && pos_ok(a, pl, pos[u]);
     const float T = wave_kth_smallest(ok[0] ? d[0] : kInf, k, lane);
     const uint64_t lt = (1ull << lane) - 1;
     int total = 0;
@@ -2396,7 +2425,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     if (R >= 2 && L <= 64 * B && __builtin_amdgcn_ballot_w64(any) == 0) break;  // wave-uniform
 #pragma unroll
     for (int b = 0; b < B; b++) {
-      const bool maybe = pos[b] >= 0 && d[b] <= tk.td;
+      const bool maybe = pos_ok(a, pl, pos[b]) && d[b] <= tk.td;
       int64_t id = kSentinelId;
       if (maybe) id = a.ids[pos[b]];
       const bool pass = maybe && lexless(d[b], id, tk.td, tk.ti);
@@ -2461,7 +2490,11 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int j = t * 64 + lane;
-    const int n = (j < L && ((qm >> (j >> 2)) & 1)) ? min(pl.partN[qb + j], k) : 0;
+    int n = (j < L && ((qm >> (j >> 2)) & 1)) ? pl.partN[qb + j] : 0;
+    if (n < 0 || n > k) {  // a partial list holds at most k entries
+      atomicAdd(pl.err, 1);
+      n = 0;
+    }
     lens[j] = n;
     C += n;
   }
@@ -2617,7 +2650,8 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   while (P < C) P <<= 1;
   for (int e = lane; e < P; e += 64) {
     if (e < C) {
-      cl[e] = a.ids[cl[e]];
+      const int64_t pos = cl[e];
+      cl[e] = pos_ok(a, pl, pos) ? a.ids[pos] : kSentinelId;
     } else {
       cd[e] = kInf;
       cl[e] = kSentinelId;

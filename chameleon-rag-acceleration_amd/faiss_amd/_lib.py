@@ -32,7 +32,14 @@ SIGNATURES = {
     "ivfpq_free": (ctypes.c_int, [c_handle]),
     "ivfpq_train": (ctypes.c_int, [c_handle, ctypes.c_int64, c_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]),
     "ivfpq_add": (ctypes.c_int, [c_handle, ctypes.c_int64, c_f32p, c_i64p]),
-    "ivfpq_precompute_tables_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "ivfpq_precompute_tables_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "ivfpq_search_preassigned_tables_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
+                                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                              ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
+    "ivfpq_set_inflight": (ctypes.c_int, [c_handle, ctypes.c_int]),
+    "ivfpq_get_inflight": (ctypes.c_int, [c_handle]),
+    "ivfpq_get_error_count": (ctypes.c_int, [c_handle, c_i64p]),
     "ivfpq_add_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
     "ivfpq_add_preencoded": (ctypes.c_int, [c_handle, ctypes.c_int64, c_i64p, c_u8p, c_i64p]),

@@ -195,6 +195,21 @@ class _InvertedLists:
     def get_codes(self, l):
         return self._get(l)[0].reshape(-1)
 
+    def export(self):
+        """All lists at once: (list_no int64 [ntotal], codes uint8 [ntotal][M], ids
+        int64 [ntotal]) in list order (each list in its stored order), the input of
+        add_preencoded -- one list-size query instead of one per list."""
+        sizes = self.list_sizes()
+        tot = int(sizes.sum())
+        codes = np.empty((tot, self._o.M), np.uint8)
+        ids = np.empty(tot, np.int64)
+        off = np.concatenate([[0], np.cumsum(sizes)])
+        L = _lib.load()
+        for l in np.nonzero(sizes)[0]:
+            _lib.check(L.ivfpq_get_list(self._o._h, int(l), _ptr(codes[off[l]:], _lib.c_u8p),
+                                        _ptr(ids[off[l]:], _lib.c_i64p)))
+        return np.repeat(np.arange(self._o.nlist, dtype=np.int64), sizes), codes, ids
+
     def get_ids(self, l):
         return self._get(l)[1]
 
@@ -468,15 +483,32 @@ class IndexIVFPQ:
 
         return stream if stream is not None else torch.cuda.current_stream(x.device).cuda_stream
 
+    @property
+    def inflight(self):
+        """Batches in flight: True lets device searches issued on different
+        streams overlap (each stream keeps its own workspace, up to three);
+        False (default, unless IVFPQ_INFLIGHT=1 at creation) orders each search
+        after those still in flight on other streams.  Results are the same."""
+        return bool(_lib.load().ivfpq_get_inflight(self._h))
+
+    @inflight.setter
+    def inflight(self, on):
+        _lib.check(_lib.load().ivfpq_set_inflight(self._h, int(bool(on))))
+
+    def error_count(self):
+        """Index-check violations counted by the merge kernels since creation
+        (ivfpq_get_error_count; 0 on a correct run).  Waits for in-flight searches."""
+        out = ctypes.c_int64(0)
+        _lib.check(_lib.load().ivfpq_get_error_count(self._h, ctypes.byref(out)))
+        return out.value
+
     def search_device(self, x, k, D=None, I=None, stream=None):
         """Search with inputs resident in HBM.  ``x`` is a torch float32 CUDA
         tensor [n, d] on the index's device; returns torch (D, I) there, launched
         on ``stream`` (default: torch's current stream).  Searches of one index
         may be issued on different streams without synchronizing: the library
-        orders each search after those still in flight on other streams.  With
-        IVFPQ_INFLIGHT=1 in the environment (experimental) the handle's
-        per-stream workspaces (up to three) let batches on different streams
-        overlap instead."""
+        orders each search after those still in flight on other streams, or,
+        with ``inflight`` on, lets them overlap."""
         import torch
 
         self._check_k(k)
@@ -486,7 +518,10 @@ class IndexIVFPQ:
                                                    I.data_ptr(), ctypes.c_void_p(self._stream(x, stream))))
         return D, I
 
-    def search_preassigned_device(self, x, k, Iq, Dq=None, D=None, I=None, stream=None):
+    def search_preassigned_device(self, x, k, Iq, Dq=None, D=None, I=None, stream=None, tables=None):
+        """search_preassigned with HBM-resident inputs.  ``tables``: the token of a
+        ``precompute_tables_device(x)`` call for exactly these queries, whose T3
+        this search consumes instead of building its own."""
         import torch
 
         self._check_k(k)
@@ -496,21 +531,30 @@ class IndexIVFPQ:
         if Dq is not None:
             self._check_dev(Dq, "Dq", torch.float32, (n, self.nprobe))
         D, I = self._dev_outputs(x, k, D, I)
-        _lib.check(_lib.load().ivfpq_search_preassigned_device(
-            self._h, n, x.data_ptr(), int(k), Iq.data_ptr(), Dq.data_ptr() if Dq is not None else None,
-            D.data_ptr(), I.data_ptr(), ctypes.c_void_p(self._stream(x, stream))))
+        if tables is not None:
+            _lib.check(_lib.load().ivfpq_search_preassigned_tables_device(
+                self._h, n, x.data_ptr(), int(k), Iq.data_ptr(), Dq.data_ptr() if Dq is not None else None,
+                D.data_ptr(), I.data_ptr(), ctypes.c_uint64(int(tables)), ctypes.c_void_p(self._stream(x, stream))))
+        else:
+            _lib.check(_lib.load().ivfpq_search_preassigned_device(
+                self._h, n, x.data_ptr(), int(k), Iq.data_ptr(), Dq.data_ptr() if Dq is not None else None,
+                D.data_ptr(), I.data_ptr(), ctypes.c_void_p(self._stream(x, stream))))
         return D, I
 
     def precompute_tables_device(self, x, stream=None):
-        """T3 of the queries x (torch CUDA [n, d]) on ``stream``, for the next
-        search_preassigned_device of exactly this tensor: the shard flow runs it
-        on a side stream while the coarse step and the probe all-gather run."""
+        """T3 of the queries x (torch CUDA [n, d]) on ``stream``; returns the token
+        that ``search_preassigned_device(x, ..., tables=token)`` consumes.  The
+        shard flow runs it on a side stream while the coarse step and the probe
+        all-gather run.  Up to three tokens can be pending."""
         import torch
 
         n = x.shape[0] if x.dim() == 2 else -1
         self._check_dev(x, "x", torch.float32, (n, self.d))
+        tok = ctypes.c_uint64(0)
         _lib.check(_lib.load().ivfpq_precompute_tables_device(self._h, n, x.data_ptr(),
-                                                              ctypes.c_void_p(self._stream(x, stream))))
+                                                              ctypes.c_void_p(self._stream(x, stream)),
+                                                              ctypes.byref(tok)))
+        return tok.value
 
     def add_device(self, x, ids=None, stream=None):
         """add / add_with_ids with the vectors already in HBM (torch float32 CUDA

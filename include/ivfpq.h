@@ -18,8 +18,13 @@
  * RuntimeError, as Faiss's SWIG wrapper does for FaissException).
  * Thread-safety: one mutex per handle; train/add/search serialize on it.
  * Stream ordering: a handle's device searches may be issued on different
- * streams without synchronizing; each one waits (hipStreamWaitEvent) for the
- * previous search on the handle, whose workspaces it reuses.
+ * streams without synchronizing.  By default each one waits (hipStreamWaitEvent)
+ * for every search of the handle still in flight on another stream.  With
+ * batches in flight on (ivfpq_set_inflight, or IVFPQ_INFLIGHT=1 in the
+ * environment when the handle is created) searches on up to three streams
+ * overlap, each in the per-stream workspace it last used; a fourth stream takes
+ * over the least recently used workspace after waiting on the host for its
+ * last search.  Results are identical in both modes.
  */
 #ifndef CHAMELEON_IVFPQ_H
 #define CHAMELEON_IVFPQ_H
@@ -109,17 +114,35 @@ int ivfpq_search_preassigned_device(ivfpq_index* h, int64_t n, const float* x, i
 int ivfpq_serve_request(ivfpq_index* h, const uint8_t* msg, int64_t msg_len, int with_lists, int batch_size, int dim,
                         int nprobe, uint8_t* answer, int64_t answer_cap, int64_t* answer_len);
 
-/* The inner-product tables T3 of n HBM-resident queries, computed on `stream`
- * ahead of a search_preassigned_device of exactly those queries (same pointer
- * and n), which then uses them instead of building its own.  The shard flow
- * issues it on a side stream while the coarse step and the probe all-gather run
- * (T3 depends only on the queries).  Tables are consumed in order: a search takes
- * the oldest pending tables of its queries (pointer, n and contents unchanged
- * since the call) and drops older ones; a search matching none drops all.  Up to
- * three can be pending, so a shard loop can keep batches in flight.
- * Reference: IndexIVFPQ::search_preassigned's
- * per-query precompute_list_tables (bench_gpu_1bn.py:605-616 shard step). */
-int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream);
+/* The inner-product tables T3 of n HBM-resident queries (1 <= n <= 16384 at M=16:
+ * one 256 MB table buffer), computed on `stream` ahead of the preassigned search
+ * of those queries.  *token receives the handle that search passes to
+ * ivfpq_search_preassigned_tables_device, which consumes the tables (the queries
+ * x must be unchanged in between).  The shard flow issues it on a side stream
+ * while the coarse step and the probe all-gather run (T3 depends only on the
+ * queries).  Up to three tables can be pending, so a shard loop can keep batches
+ * in flight; a fourth precompute overwrites the oldest pending one (its token is
+ * then rejected).  Training, set_trained and reset drop pending tables.
+ * ivfpq_search_preassigned_device never uses precomputed tables.
+ * Reference: IndexIVFPQ::search_preassigned's per-query precompute_list_tables
+ * (bench_gpu_1bn.py:605-616 shard step). */
+int ivfpq_precompute_tables_device(ivfpq_index* h, int64_t n, const float* x, void* stream, uint64_t* token);
+int ivfpq_search_preassigned_tables_device(ivfpq_index* h, int64_t n, const float* x, int k, const int64_t* Iq,
+                                           const float* Dq, float* D, int64_t* I, uint64_t token, void* stream);
+
+/* Batches in flight (see "Stream ordering" above): 1 = device searches on different
+ * streams overlap, 0 = each waits for the others (default, unless IVFPQ_INFLIGHT=1).
+ * Waits for the handle's in-flight searches before switching.  Reference: the query
+ * blocks streamed through one GPU index, bench_gpu_1bn.py:788-806. */
+int ivfpq_set_inflight(ivfpq_index* h, int on);
+int ivfpq_get_inflight(const ivfpq_index* h);
+
+/* Index checks of the merge kernels: code positions read back from partial lists
+ * outside the image, partial-list lengths above k and pair ids outside the batch
+ * are counted (and dropped, never dereferenced).  *out = the count since the
+ * handle was created, over all its workspaces, after waiting for in-flight
+ * searches.  0 on a correct run; the tests assert it. */
+int ivfpq_get_error_count(ivfpq_index* h, int64_t* out);
 
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing

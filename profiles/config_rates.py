@@ -48,6 +48,7 @@ def rate(ix, xq_dev, k, reps):
     # between device-wide synchronisations), as bench.py's timed region
     ss = [torch.cuda.Stream() for _ in range(2)]
     outs = [(D, I), (torch.empty_like(D), torch.empty_like(I))]
+    ix.inflight = True
     for r in range(4):  # warm: each stream's workspace allocated before timing
         ix.search_device(xq_dev[(r % nb) * B:(r % nb + 1) * B], k, *outs[r % 2], stream=ss[r % 2].cuda_stream)
     torch.cuda.synchronize()
@@ -57,6 +58,7 @@ def rate(ix, xq_dev, k, reps):
         ix.search_device(xq_dev[b * B:(b + 1) * B], k, *outs[r % 2], stream=ss[r % 2].cuda_stream)
     torch.cuda.synchronize()
     ms2 = (time.perf_counter() - t0) * 1000.0 / reps
+    ix.inflight = False
     return {"k": k, "ms_per_batch": ms, "queries_per_s": B / (ms * 1e-3),
             "ms_per_batch_inflight2": ms2, "queries_per_s_inflight2": B / (ms2 * 1e-3)}
 

@@ -71,10 +71,10 @@ def main():
             e[0].record()
             # T3 of the global batch on a side stream, concurrent with the coarse step (bench.py's shard flow)
             side.wait_stream(torch.cuda.current_stream())
-            sh.precompute_tables_device(xg, stream=side.cuda_stream)
+            tok = sh.precompute_tables_device(xg, stream=side.cuda_stream)
             sh.coarse_device(xg[:B])
             e[1].record()
-            Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all)
+            Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, tables=tok)
             e[2].record()
             faiss.merge_topk_device(torch.stack([Dp[:B]] * N), torch.stack([Ip[:B]] * N))
             e[3].record()
@@ -94,13 +94,14 @@ def main():
         def rank_step(j):
             with torch.cuda.stream(comp[j]):
                 sides[j].wait_stream(comp[j])
-                sh.precompute_tables_device(xg, stream=sides[j].cuda_stream)
+                tok = sh.precompute_tables_device(xg, stream=sides[j].cuda_stream)
                 sh.coarse_device(xg[:B])
-                Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j])
+                Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j], tables=tok)
                 faiss.merge_topk_device(torch.stack([Dp[:B]] * N), torch.stack([Ip[:B]] * N))
 
         wall = {}
         for label, depth in (("serial", 1), ("inflight2", 2)):
+            sh.inflight = depth > 1
             for s in range(4):
                 rank_step(s % depth)
             torch.cuda.synchronize()

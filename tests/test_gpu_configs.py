@@ -1,7 +1,8 @@
 """GPU parity at the BASELINE.json config shapes (C1-C4) and for the list-range
 shard path, through the C-ABI, bit-exact against the CPU oracle.
 
-* C1 / C2: the SIFT1M-shaped index (nb = 1e6, IVF1024,PQ16) at nprobe 8 and 16.
+* C1 / C2: bench.py's SIFT1M-shaped index (nb = 1e6, IVF1024,PQ16, 200k-centre
+  data, 25 + 25 training iterations) at nprobe 8 and 16.
 * C3-shaped: d = 768, M = 64 (64-B codes), nprobe = 32, k in {10, 1000}, at a
   reduced base size (the kernels' M = 64 instantiations).
 * C4-shaped: d = 96, M = 48 (dsub 2), nlist = 65536 (the large-nlist coarse
@@ -55,7 +56,8 @@ def build(d, nlist, M, nb, nt, nq, niter, metric=faiss.METRIC_L2, n_centres=1000
 
 @pytest.fixture(scope="module")
 def sift1m():
-    ix, xq = build(128, 1024, 16, 1_000_000, 100_000, 1024, 8)
+    # bench.py's C2 index exactly: 200k-centre data, 25 + 25 training iterations
+    ix, xq = build(128, 1024, 16, 1_000_000, 100_000, 1024, 25, n_centres=200_000)
     return ix, oracle_like(ix), xq
 
 
@@ -317,9 +319,12 @@ def test_c4_shape_eight_list_range_shards(c4_shape, k):
 def test_precomputed_tables_on_a_side_stream(sift1m):
     """bench.py's shard step computes T3 of the global batch on a side stream
     (precompute_tables_device) while the coarse step runs; the preassigned search
-    of exactly those queries then uses it.  Results equal the plain preassigned
+    given that call's token then uses it.  Results equal the plain preassigned
     search and the oracle, over several back-to-back steps (the next step's T3
-    is ordered after the previous search that read the buffer)."""
+    is ordered after the previous search that read the buffer).  Tables are
+    handed over only by token: a search without one never uses pending tables,
+    a consumed, overwritten or mis-sized token is rejected, and retraining drops
+    pending tables."""
     import torch
 
     ix, ox, xq = sift1m
@@ -330,22 +335,44 @@ def test_precomputed_tables_on_a_side_stream(sift1m):
     side = torch.cuda.Stream()
     for step in range(3):
         side.wait_stream(torch.cuda.current_stream())
-        ix.precompute_tables_device(xd, stream=side.cuda_stream)
-        D, I = ix.search_preassigned_device(xd, 10, Iq, Dq)
+        tok = ix.precompute_tables_device(xd, stream=side.cuda_stream)
+        D, I = ix.search_preassigned_device(xd, 10, Iq, Dq, tables=tok)
         torch.cuda.synchronize()
         assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
-    # tables of another batch are not used for this one
-    ix.precompute_tables_device(xd[:512].contiguous(), stream=side.cuda_stream)
+        with pytest.raises(RuntimeError, match="not pending"):  # consumed
+            ix.search_preassigned_device(xd, 10, Iq, Dq, tables=tok)
+    # tables of other queries, pending under the same pointer, are not used by a search without the token
+    x2 = torch.from_numpy(xq[::-1].copy()).cuda()
+    xd_alias = xd.clone()
+    xd.copy_(x2)
+    tok = ix.precompute_tables_device(xd, stream=side.cuda_stream)
+    xd.copy_(xd_alias)
+    torch.cuda.synchronize()
     D, I = ix.search_preassigned_device(xd, 10, Iq, Dq)
     torch.cuda.synchronize()
     assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+    with pytest.raises(RuntimeError, match="computed for"):  # token of n queries used for another n
+        ix.search_preassigned_device(xd[:512].contiguous(), 10, Iq[:512].contiguous(), Dq[:512].contiguous(),
+                                     tables=tok)
+    # a fourth pending precompute overwrites the oldest token
+    toks = [ix.precompute_tables_device(xd, stream=side.cuda_stream) for _ in range(3)]
+    with pytest.raises(RuntimeError, match="not pending"):
+        ix.search_preassigned_device(xd, 10, Iq, Dq, tables=tok)
+    D, I = ix.search_preassigned_device(xd, 10, Iq, Dq, tables=toks[0])
+    torch.cuda.synchronize()
+    assert_same(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+    ix.set_trained(ix.centroids(), ix.codebook())  # new quantizers: pending tables are dropped
+    with pytest.raises(RuntimeError, match="not pending"):
+        ix.search_preassigned_device(xd, 10, Iq, Dq, tables=toks[1])
+    assert ix.error_count() == 0
 
 
-def test_precomputed_tables_with_batches_in_flight(sift1m):
-    """The shard step pipelined: 8 batches (4 distinct query sets, so tables of
-    the same pointer recur) issued on 2 compute streams, each with its own side
-    stream for the T3 ahead, and with the T3 of batch s + 1 issued before the
-    search of batch s (tables consumed in order), with no synchronisation.
+@pytest.mark.parametrize("inflight", [False, True])
+def test_precomputed_tables_with_batches_in_flight(sift1m, inflight):
+    """The shard step pipelined: 8 batches (4 distinct query sets) issued on 2
+    compute streams, each with its own side stream for the T3 ahead, and with the
+    T3 of batch s + 1 issued before the search of batch s, with no
+    synchronisation, in both stream modes (ordered, and batches in flight).
     Every batch equals its plain preassigned search."""
     import torch
 
@@ -361,17 +388,22 @@ def test_precomputed_tables_with_batches_in_flight(sift1m):
         ref.append((D.cpu().numpy(), I.cpu().numpy()))
     comp = [torch.cuda.Stream() for _ in range(2)]
     side = [torch.cuda.Stream() for _ in range(2)]
-    torch.cuda.synchronize()
-    outs = []
-    ix.precompute_tables_device(xs[0], stream=side[0].cuda_stream)
-    for s in range(8):
-        j = s % 2
-        x = xs[s % 4]
-        if s + 1 < 8:  # the next batch's tables first
-            ix.precompute_tables_device(xs[(s + 1) % 4], stream=side[(s + 1) % 2].cuda_stream)
-        with torch.cuda.stream(comp[j]):
-            Dq, Iq = ix.coarse_device(x)
-            outs.append(ix.search_preassigned_device(x, 10, Iq, Dq))
-    torch.cuda.synchronize()
+    ix.inflight = inflight
+    try:
+        torch.cuda.synchronize()
+        outs = []
+        toks = {0: ix.precompute_tables_device(xs[0], stream=side[0].cuda_stream)}
+        for s in range(8):
+            j = s % 2
+            x = xs[s % 4]
+            if s + 1 < 8:  # the next batch's tables first
+                toks[s + 1] = ix.precompute_tables_device(xs[(s + 1) % 4], stream=side[(s + 1) % 2].cuda_stream)
+            with torch.cuda.stream(comp[j]):
+                Dq, Iq = ix.coarse_device(x)
+                outs.append(ix.search_preassigned_device(x, 10, Iq, Dq, tables=toks[s]))
+        torch.cuda.synchronize()
+    finally:
+        ix.inflight = False
     for s, (D, I) in enumerate(outs):
         assert_same(D.cpu().numpy(), I.cpu().numpy(), *ref[s % 4])
+    assert ix.error_count() == 0

@@ -251,28 +251,38 @@ def test_device_searches_on_two_streams_without_sync(golden_dir):
         assert_same(D3, I3, z["or_D"], z["or_I"])
 
 
-def test_batches_in_flight_on_round_robin_streams():
-    """12 batches issued round robin on 4 streams with no synchronisation (more
-    streams than the handle's 3 workspaces, so workspaces are reused across
-    streams; the library orders the searches across streams), at k = 10 (row-packed scan) and k = 100 (k > 64
-    merge), with a coarse_device + preassigned search interleaved.  Every batch
-    equals its serial search on one stream, bit for bit; the serial results are
-    themselves checked against the oracle for the first batch."""
-    import torch
-
+@pytest.fixture(scope="module")
+def rr_index():
     xt = datasets.synthetic_sift_like(20_000, 64, seed=4321, n_centres=20_000)
     xb = datasets.synthetic_sift_like(100_000, 64, seed=1234, n_centres=20_000)
-    xq = datasets.synthetic_sift_like(12 * 256, 64, seed=123, n_centres=20_000)
+    xq = datasets.synthetic_sift_like(24 * 256, 64, seed=123, n_centres=20_000)
     ix = faiss.index_factory(64, "IVF256,PQ8", device=0)
     ix.niter_coarse = ix.niter_pq = 8
     ix.train(xt)
     ix.add(xb)
     ix.nprobe = 12
-    xd = torch.from_numpy(xq).cuda().view(12, 256, 64)
+    return ix, xq
+
+
+@pytest.mark.parametrize("inflight", [False, True])
+def test_batches_in_flight_on_round_robin_streams(rr_index, inflight):
+    """24 batches issued round robin on 2, 3, 4 and 5 streams with no
+    synchronisation, at k = 10 (row-packed scan) and k = 100 (k > 64 merge), with
+    a coarse_device + preassigned search interleaved, in both stream modes:
+    searches ordered across streams, and batches in flight (up to three
+    overlapping in per-stream workspaces; 4 and 5 streams take workspaces over).
+    Every batch equals its search alone on one stream, bit for bit (those are
+    checked against the oracle for the first batch), and the merge kernels'
+    index checks count nothing."""
+    import torch
+
+    ix, xq = rr_index
+    nb = 24
+    xd = torch.from_numpy(xq).cuda().view(nb, 256, 64)
     torch.cuda.synchronize()
     for k in (10, 100):
         ref = []
-        for b in range(12):
+        for b in range(nb):
             D, I = ix.search_device(xd[b], k)
             torch.cuda.synchronize()
             ref.append((D.cpu().numpy(), I.cpu().numpy()))
@@ -286,24 +296,30 @@ def test_batches_in_flight_on_round_robin_streams():
             ox.nprobe = 12
             Do, Io = ox.search(xq[:256], k, 4)
             assert_same(ref[0][0], ref[0][1], Do, Io)
-        streams = [torch.cuda.Stream() for _ in range(4)]
-        outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
-                for _ in range(12)]
-        pre = None
-        torch.cuda.synchronize()
-        for b in range(12):
-            st = streams[b % 4].cuda_stream
-            if b == 5:  # a coarse step + preassigned search in the middle of the pipeline
-                with torch.cuda.stream(streams[b % 4]):
-                    Dq, Iq = ix.coarse_device(xd[b], stream=st)
-                    pre = ix.search_preassigned_device(xd[b], k, Iq, Dq, stream=st)
-            ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=st)
-        torch.cuda.synchronize()
-        for b in range(12):
-            np.testing.assert_array_equal(outs[b][1].cpu().numpy(), ref[b][1])
-            np.testing.assert_array_equal(outs[b][0].cpu().numpy(), ref[b][0])
-        np.testing.assert_array_equal(pre[1].cpu().numpy(), ref[5][1])
-        np.testing.assert_array_equal(pre[0].cpu().numpy(), ref[5][0])
+        for nst in (2, 3, 4, 5):
+            streams = [torch.cuda.Stream() for _ in range(nst)]
+            outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
+                    for _ in range(nb)]
+            pre = None
+            ix.inflight = inflight
+            try:
+                torch.cuda.synchronize()
+                for b in range(nb):
+                    st = streams[b % nst].cuda_stream
+                    if b == 5:  # a coarse step + preassigned search in the middle of the pipeline
+                        with torch.cuda.stream(streams[b % nst]):
+                            Dq, Iq = ix.coarse_device(xd[b], stream=st)
+                            pre = ix.search_preassigned_device(xd[b], k, Iq, Dq, stream=st)
+                    ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=st)
+                torch.cuda.synchronize()
+            finally:
+                ix.inflight = False
+            for b in range(nb):
+                np.testing.assert_array_equal(outs[b][1].cpu().numpy(), ref[b][1], err_msg=f"k={k} streams={nst} b={b}")
+                np.testing.assert_array_equal(outs[b][0].cpu().numpy(), ref[b][0], err_msg=f"k={k} streams={nst} b={b}")
+            np.testing.assert_array_equal(pre[1].cpu().numpy(), ref[5][1])
+            np.testing.assert_array_equal(pre[0].cpu().numpy(), ref[5][0])
+    assert ix.error_count() == 0
 
 
 def test_device_entry_points_reject_bad_tensors(golden_dir):
