@@ -31,4 +31,27 @@ hipError_t image_merge_sort(const ImageMergeArgs& g, void* scratch, size_t scrat
 hipError_t image_merge_gather(const ImageMergeArgs& g, int64_t n_out, void* scratch, hipStream_t s);
 void launch_iota_i64(int64_t* v, int64_t n, int64_t start, hipStream_t s);
 
+// Per-list merge of a new image (new_off / new_codes / new_ids: entries sorted by
+// (list, label), e.g. the output of image_merge_sort + image_merge_gather over the
+// new entries alone) into the current image: out_off = old_off + new_off, and
+// every list of [lo, hi) interleaved by label, old entries first on equal labels
+// -- the image a full re-sort of old + new gives, built by moving each entry once
+// (no sort of the old entries).  max_list: the largest old + new list length.
+struct ListMergeArgs {
+  int nlist = 0, lo = 0, hi = 0, M = 0;
+  int64_t max_list = 0;
+  const int64_t* old_off = nullptr;
+  const uint8_t* old_codes = nullptr;
+  const int64_t* old_ids = nullptr;
+  const int64_t* new_off = nullptr;
+  const uint8_t* new_codes = nullptr;
+  const int64_t* new_ids = nullptr;
+  int64_t* out_off = nullptr;
+  uint8_t* out_codes = nullptr;
+  int64_t* out_ids = nullptr;
+};
+hipError_t image_merge_lists(const ListMergeArgs& g, hipStream_t s);
+// *count += entries of lists[0, n) inside [lo, hi)
+hipError_t count_kept(const int64_t* lists, int64_t n, int lo, int hi, unsigned long long* count, hipStream_t s);
+
 }  // namespace chivf

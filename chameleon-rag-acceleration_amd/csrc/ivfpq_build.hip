@@ -171,6 +171,105 @@ hipError_t image_merge_gather(const ImageMergeArgs& g, int64_t n_out, void* scra
   return hipGetLastError();
 }
 
+// ---- per-list merge of a sorted new image into the current one ---------------
+namespace {
+
+// out_off[l] = old_off[l] + new_off[l]  (both are list prefixes; l in [0, nlist])
+__global__ __launch_bounds__(256) void k_sum_offsets(const int64_t* __restrict__ a, const int64_t* __restrict__ b,
+                                                     int n, int64_t* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i <= n) out[i] = a[i] + b[i];
+}
+
+// first index in v[0, n) with v[i] >= x (lower) or > x (upper)
+__device__ __forceinline__ int64_t bsearch_i64(const int64_t* __restrict__ v, int64_t n, int64_t x, bool upper) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (upper ? v[mid] <= x : v[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void copy_code(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, int M) {
+  if ((M & 15) == 0) {
+    for (int v = 0; v < M / 16; v++) reinterpret_cast<uint4*>(d)[v] = reinterpret_cast<const uint4*>(s)[v];
+  } else if ((M & 7) == 0) {
+    for (int v = 0; v < M / 8; v++) reinterpret_cast<uint2*>(d)[v] = reinterpret_cast<const uint2*>(s)[v];
+  } else {
+    for (int v = 0; v < M; v++) d[v] = s[v];
+  }
+}
+
+// One workgroup per (list, 64 Ki-entry tile): list l's old entries O (label-sorted)
+// and new entries N (label-sorted) interleaved by label into the output list, old
+// before new on equal labels (the stable (list, label) order of a full re-sort of
+// old + new).  Old entry r lands at r + |{n in N : n < label_r}|, new entry t at
+// t + |{o in O : o <= label_t}|; when every new label is above the old ones (ids
+// assigned sequentially) both counts are trivial and the list is an append.
+constexpr int kTile = 65536;
+__global__ __launch_bounds__(256) void k_merge_lists(int lo, const int64_t* __restrict__ old_off,
+                                                     const uint8_t* __restrict__ old_codes,
+                                                     const int64_t* __restrict__ old_ids,
+                                                     const int64_t* __restrict__ new_off,
+                                                     const uint8_t* __restrict__ new_codes,
+                                                     const int64_t* __restrict__ new_ids,
+                                                     const int64_t* __restrict__ out_off, int M,
+                                                     uint8_t* __restrict__ out_codes, int64_t* __restrict__ out_ids) {
+  const int l = lo + blockIdx.y;
+  const int64_t ob = old_off[l], no = old_off[l + 1] - ob;
+  const int64_t nb = new_off[l], nn = new_off[l + 1] - nb;
+  const int64_t t0 = (int64_t)blockIdx.x * kTile;
+  if (t0 >= no + nn) return;
+  const int64_t dst = out_off[l];
+  const int64_t* O = old_ids + ob;
+  const int64_t* N = new_ids + nb;
+  const bool append = nn == 0 || no == 0 || O[no - 1] < N[0];
+  const int64_t t1 = min(t0 + kTile, no + nn);
+  for (int64_t e = t0 + threadIdx.x; e < t1; e += 256) {
+    if (e < no) {  // old entry r = e
+      const int64_t lab = O[e];
+      const int64_t at = dst + e + (append ? 0 : bsearch_i64(N, nn, lab, false));
+      copy_code(out_codes + at * M, old_codes + (ob + e) * M, M);
+      out_ids[at] = lab;
+    } else {  // new entry t = e - no
+      const int64_t t = e - no;
+      const int64_t lab = N[t];
+      const int64_t at = dst + t + (append ? no : bsearch_i64(O, no, lab, true));
+      copy_code(out_codes + at * M, new_codes + (nb + t) * M, M);
+      out_ids[at] = lab;
+    }
+  }
+}
+
+// entries of `lists` inside [lo, hi) (the ones a list-range shard keeps), added to *count
+__global__ __launch_bounds__(256) void k_count_kept(const int64_t* __restrict__ lists, int64_t n, int lo, int hi,
+                                                    unsigned long long* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool keep = i < n && lists[i] >= lo && lists[i] < hi;
+  const unsigned long long m = __ballot(keep);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned long long)__popcll(m));
+}
+
+}  // namespace
+
+hipError_t image_merge_lists(const ListMergeArgs& g, hipStream_t s) {
+  hipLaunchKernelGGL(k_sum_offsets, dim3(nblk(g.nlist + 1, 256)), dim3(256), 0, s, g.old_off, g.new_off, g.nlist,
+                     g.out_off);
+  if (g.hi > g.lo && g.max_list > 0) {
+    const dim3 grid((unsigned)((g.max_list + kTile - 1) / kTile), (unsigned)(g.hi - g.lo));
+    hipLaunchKernelGGL(k_merge_lists, grid, dim3(256), 0, s, g.lo, g.old_off, g.old_codes, g.old_ids, g.new_off,
+                       g.new_codes, g.new_ids, g.out_off, g.M, g.out_codes, g.out_ids);
+  }
+  return hipGetLastError();
+}
+
+hipError_t count_kept(const int64_t* lists, int64_t n, int lo, int hi, unsigned long long* count, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_count_kept, dim3(nblk(n, 256)), dim3(256), 0, s, lists, n, lo, hi, count);
+  return hipGetLastError();
+}
+
 void launch_iota_i64(int64_t* v, int64_t n, int64_t start, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(k_iota_i64, dim3(nblk(n, 256)), dim3(256), 0, s, v, n, start);
 }

@@ -186,8 +186,12 @@ struct ivfpq_index {
   // scratch
   DevBuf w_x, w_xn, w_D, w_I, w_lno, w_codes, w_cent, w_cn;
   DevBuf h_D, h_I, h_Iq, h_Dq;  // device staging of the host-buffer entry points
-  // device-side add: the new entries of one add call, and the image merge scratch
-  DevBuf a_lists, a_ids, a_codes, a_scratch, a_off;
+  // device-side adds not yet merged into the image (add_dev / flush_pending): list
+  // numbers (any list; entries outside [list_lo, list_hi) are dropped at the merge),
+  // labels and codes, q_n of them (q_kept inside the range); a_off: small scratch
+  DevBuf q_lists, q_ids, q_codes, a_off;
+  int64_t q_n = 0, q_kept = 0, q_cap = 0;
+  int64_t img_n = 0;  // entries in the device image (ntotal = img_n + q_kept)
   bool host_stale = false;  // the device image holds entries the host lists lack (device-side adds)
   // T3 of a batch computed ahead (ivfpq_precompute_tables_device), handed to a
   // preassigned search by the token that call returned (seq)
@@ -486,6 +490,7 @@ struct ivfpq_index {
   }
 
   void upload_lists() {
+    flush_pending(stream);
     if (!dirty) return;
     quiesce();  // in-flight searches may still read the old device lists
     std::vector<int64_t> off(nlist + 1, 0);
@@ -521,6 +526,7 @@ struct ivfpq_index {
     }
     HIPCHECK(hipMemcpyAsync(d_off.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, stream));
     HIPCHECK(hipStreamSynchronize(stream));
+    img_n = tot;
     dirty = false;
   }
 
@@ -528,6 +534,7 @@ struct ivfpq_index {
   // order: each list label-sorted.
   void sync_host() {
     if (!host_stale) return;
+    flush_pending(stream);
     quiesce();
     std::vector<int64_t> off(nlist + 1);
     HIPCHECK(hipMemcpy(off.data(), d_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToHost));
@@ -547,19 +554,25 @@ struct ivfpq_index {
 
   // Device-side add of n vectors (x on the host or the device; ids nullable =
   // sequential): coarse assignment on the matrix cores (the search's coarse
-  // kernels, top-1), PQ encode, then one merge of the new entries into the
-  // device image (ivfpq_build.hip).  No per-chunk host synchronization.
+  // kernels, top-1) and PQ encode into the pending set (q_*), no per-chunk host
+  // synchronization.  The pending set is merged into the image (flush_pending)
+  // before the lists are next read, or once it holds as many entries as the
+  // image: every entry is then moved O(1) times over any sequence of adds
+  // (Chameleon adds a 1e9 base in 1e6 slices, bench_gpu_1bn.py:598-658; beir in
+  // 50k chunks, faiss_index.py:40-42), instead of the whole image being
+  // re-sorted at every add.
   void add_dev(int64_t n, const float* x, bool x_on_device, const int64_t* ids, bool ids_on_device, hipStream_t s) {
     require(trained, "index is not trained");
     if (n <= 0) return;
     upload_lists();  // host-side adds not yet in the image
     order_after_all(s);
     quiesce();
+    // the pending sort permutes entries with 32-bit indices
+    require(q_n + n < (int64_t(1) << 32) - 1, "more than 2^32 - 2 vectors pending in one merge");
     const int64_t rows = nlist >= kSegmentedNlist ? std::min<int64_t>(n, 1 << 18)
                                                   : std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
-    a_lists.ensure(sizeof(int64_t) * n);
-    a_codes.ensure((size_t)n * M);
-    a_ids.ensure(sizeof(int64_t) * n);
+    pend_reserve(q_n + n, s);
+    int64_t* lists = q_lists.as<int64_t>() + q_n;
     w_D.ensure(sizeof(float) * rows);
     if (!x_on_device) w_x.ensure(sizeof(float) * rows * d);
     for (int64_t r0 = 0; r0 < n; r0 += rows) {
@@ -569,62 +582,145 @@ struct ivfpq_index {
         HIPCHECK(hipMemcpyAsync(w_x.p, xd, sizeof(float) * c * d, hipMemcpyHostToDevice, s));
         xd = w_x.as<float>();
       }
-      coarse_launch(xd, c, 1, w_D.as<float>(), a_lists.as<int64_t>() + r0, s);
-      launch_pq_encode(xd, c, d, d_cent.as<float>(), a_lists.as<int64_t>() + r0, d_cb.as<float>(), M, ksub,
-                       a_codes.as<uint8_t>() + r0 * M, s);
+      coarse_launch(xd, c, 1, w_D.as<float>(), lists + r0, s);
+      launch_pq_encode(xd, c, d, d_cent.as<float>(), lists + r0, d_cb.as<float>(), M, ksub,
+                       q_codes.as<uint8_t>() + (q_n + r0) * M, s);
       HIPCHECK(hipGetLastError());
       if (!x_on_device) HIPCHECK(hipStreamSynchronize(s));  // w_x is reused by the next chunk's copy
     }
     if (!ids) {
-      launch_iota_i64(a_ids.as<int64_t>(), n, next_id, s);
+      launch_iota_i64(q_ids.as<int64_t>() + q_n, n, next_id, s);
       next_id += n;
     } else {
-      HIPCHECK(hipMemcpyAsync(a_ids.p, ids, sizeof(int64_t) * n,
+      HIPCHECK(hipMemcpyAsync(q_ids.as<int64_t>() + q_n, ids, sizeof(int64_t) * n,
                               ids_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     }
+    int64_t kept = n;
+    if (list_lo > 0 || list_hi < nlist) {  // a list-range shard keeps its own lists only
+      a_off.ensure(sizeof(unsigned long long));
+      HIPCHECK(hipMemsetAsync(a_off.p, 0, sizeof(unsigned long long), s));
+      HIPCHECK(count_kept(lists, n, list_lo, list_hi, a_off.as<unsigned long long>(), s));
+      unsigned long long k = 0;
+      HIPCHECK(hipMemcpyAsync(&k, a_off.p, sizeof(k), hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      kept = (int64_t)k;
+    } else {
+      HIPCHECK(hipStreamSynchronize(s));
+    }
+    q_n += n;
+    q_kept += kept;
+    ntotal += kept;
+    host_stale = true;
+    dirty = false;
+    if (q_n >= std::max<int64_t>(img_n, int64_t(1) << 24)) flush_pending(s);
+  }
+
+  void pend_reserve(int64_t need, hipStream_t s) {
+    if (need <= q_cap) return;
+    const int64_t cap = std::max<int64_t>(need, q_cap * 2);
+    DevBuf l2, i2, c2;
+    l2.ensure(sizeof(int64_t) * cap);
+    i2.ensure(sizeof(int64_t) * cap);
+    c2.ensure((size_t)cap * M);
+    if (q_n > 0) {
+      HIPCHECK(hipMemcpyAsync(l2.p, q_lists.p, sizeof(int64_t) * q_n, hipMemcpyDeviceToDevice, s));
+      HIPCHECK(hipMemcpyAsync(i2.p, q_ids.p, sizeof(int64_t) * q_n, hipMemcpyDeviceToDevice, s));
+      HIPCHECK(hipMemcpyAsync(c2.p, q_codes.p, (size_t)q_n * M, hipMemcpyDeviceToDevice, s));
+      HIPCHECK(hipStreamSynchronize(s));
+    }
+    std::swap(q_lists.p, l2.p);
+    std::swap(q_lists.bytes, l2.bytes);
+    std::swap(q_ids.p, i2.p);
+    std::swap(q_ids.bytes, i2.bytes);
+    std::swap(q_codes.p, c2.p);
+    std::swap(q_codes.bytes, c2.bytes);
+    q_cap = cap;
+  }
+
+  void drop_pending() {
+    q_lists.release();
+    q_ids.release();
+    q_codes.release();
+    q_n = q_kept = q_cap = 0;
+  }
+
+  // The pending entries merged into the device image: sorted by (list, label)
+  // alone (rocprim radix sorts of the pending set, out-of-range lists dropped),
+  // then interleaved list by list into the label-sorted image (ivfpq_build.h
+  // image_merge_lists).  The result equals a stable (list, label) sort of old +
+  // new, the image order of DESIGN.md §3.
+  void flush_pending(hipStream_t s) {
+    if (q_n == 0) return;
+    quiesce();  // in-flight searches read the current image
     ImageMergeArgs g;
     g.nlist = nlist;
     g.lo = list_lo;
     g.hi = list_hi;
     g.M = M;
-    g.n_old = ntotal;
-    g.old_off = d_off.as<int64_t>();
-    g.old_ids = d_ids.as<int64_t>();
-    g.old_codes = d_codes.as<uint8_t>();
-    g.n_new = n;
-    g.new_lists = a_lists.as<int64_t>();
-    g.new_ids = a_ids.as<int64_t>();
-    g.new_codes = a_codes.as<uint8_t>();
-    a_off.ensure(sizeof(int64_t) * (nlist + 1));
-    g.off_out = a_off.as<int64_t>();
-    const size_t sb = image_merge_scratch_bytes(ntotal + n, nlist);
-    a_scratch.ensure(sb);
-    HIPCHECK(image_merge_sort(g, a_scratch.p, sb, s));
-    std::vector<int64_t> off(nlist + 1);
-    HIPCHECK(hipMemcpyAsync(off.data(), a_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToHost, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    const int64_t n_out = off[nlist];
-    DevBuf codes2, ids2;
-    codes2.ensure(std::max<size_t>(16, (size_t)n_out * M));
-    ids2.ensure(std::max<size_t>(16, sizeof(int64_t) * n_out));
-    g.codes_out = codes2.as<uint8_t>();
-    g.ids_out = ids2.as<int64_t>();
-    HIPCHECK(image_merge_gather(g, n_out, a_scratch.p, s));
-    d_off.ensure(sizeof(int64_t) * (nlist + 1));
-    HIPCHECK(hipMemcpyAsync(d_off.p, a_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToDevice, s));
-    HIPCHECK(hipStreamSynchronize(s));
-    std::swap(d_codes.p, codes2.p);
-    std::swap(d_codes.bytes, codes2.bytes);
-    std::swap(d_ids.p, ids2.p);
-    std::swap(d_ids.bytes, ids2.bytes);
-    ntotal = n_out;
-    a_lists.release();
-    a_codes.release();
-    a_ids.release();
-    a_scratch.release();
-    set_list_order(off);
-    host_stale = true;
-    dirty = false;
+    g.n_old = 0;
+    g.n_new = q_n;
+    g.new_lists = q_lists.as<int64_t>();
+    g.new_ids = q_ids.as<int64_t>();
+    g.new_codes = q_codes.as<uint8_t>();
+    DevBuf new_off, out_off;
+    new_off.ensure(sizeof(int64_t) * (nlist + 1));
+    g.off_out = new_off.as<int64_t>();
+    {
+      const size_t sb = image_merge_scratch_bytes(q_n, nlist);
+      DevBuf scratch, codes_n, ids_n;
+      scratch.ensure(sb);
+      HIPCHECK(image_merge_sort(g, scratch.p, sb, s));
+      std::vector<int64_t> noff(nlist + 1), ooff(nlist + 1);
+      HIPCHECK(hipMemcpyAsync(noff.data(), new_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipMemcpyAsync(ooff.data(), d_off.p, sizeof(int64_t) * (nlist + 1), hipMemcpyDeviceToHost, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      const int64_t kept = noff[nlist];
+      require(kept == q_kept, "pending merge: kept entries disagree with the add-time count");
+      codes_n.ensure(std::max<size_t>(16, (size_t)kept * M));
+      ids_n.ensure(std::max<size_t>(16, sizeof(int64_t) * kept));
+      g.codes_out = codes_n.as<uint8_t>();
+      g.ids_out = ids_n.as<int64_t>();
+      HIPCHECK(image_merge_gather(g, kept, scratch.p, s));
+      scratch.release();
+      std::vector<int64_t> off(nlist + 1);
+      int64_t mx = 0;
+      for (int l = 0; l <= nlist; l++) {
+        off[l] = ooff[l] + noff[l];
+        if (l < nlist) mx = std::max(mx, (ooff[l + 1] - ooff[l]) + (noff[l + 1] - noff[l]));
+      }
+      const int64_t n_out = off[nlist];
+      DevBuf codes2, ids2;
+      codes2.ensure(std::max<size_t>(16, (size_t)n_out * M));
+      ids2.ensure(std::max<size_t>(16, sizeof(int64_t) * n_out));
+      out_off.ensure(sizeof(int64_t) * (nlist + 1));
+      ListMergeArgs m;
+      m.nlist = nlist;
+      m.lo = list_lo;
+      m.hi = list_hi;
+      m.M = M;
+      m.max_list = mx;
+      m.old_off = d_off.as<int64_t>();
+      m.old_codes = d_codes.as<uint8_t>();
+      m.old_ids = d_ids.as<int64_t>();
+      m.new_off = new_off.as<int64_t>();
+      m.new_codes = codes_n.as<uint8_t>();
+      m.new_ids = ids_n.as<int64_t>();
+      m.out_off = out_off.as<int64_t>();
+      m.out_codes = codes2.as<uint8_t>();
+      m.out_ids = ids2.as<int64_t>();
+      HIPCHECK(image_merge_lists(m, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      std::swap(d_codes.p, codes2.p);
+      std::swap(d_codes.bytes, codes2.bytes);
+      std::swap(d_ids.p, ids2.p);
+      std::swap(d_ids.bytes, ids2.bytes);
+      std::swap(d_off.p, out_off.p);
+      std::swap(d_off.bytes, out_off.bytes);
+      img_n = n_out;
+      set_list_order(off);
+    }
+    drop_pending();
+    require(img_n == ntotal, "pending merge: image size disagrees with ntotal");
   }
 
   // Scheduling order of the shard's lists: largest first (the list scan takes
@@ -757,7 +853,7 @@ struct ivfpq_index {
       a.codes = d_codes.as<uint8_t>();
       a.ids = d_ids.as<int64_t>();
       a.list_off = d_off.as<int64_t>();
-      a.n_codes = ntotal;
+      a.n_codes = img_n;
       a.probe_list = lists;
       a.nq = c;
       a.nprobe = np;
@@ -1108,7 +1204,10 @@ int ivfpq_reset(ivfpq_index* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     for (auto& v : h->lcodes) v.clear();
     for (auto& v : h->lids) v.clear();
+    DeviceGuard g(h->device);
+    h->quiesce();
     h->drop_tables();
+    h->drop_pending();
     h->host_stale = false;
     h->ntotal = 0;
     h->next_id = 0;
@@ -1329,6 +1428,7 @@ int ivfpq_get_list_sizes(const ivfpq_index* ch, int64_t* out) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     if (h->host_stale) {  // from the device image's offsets (no download of the lists)
+      h->flush_pending(h->stream);
       h->quiesce();
       std::vector<int64_t> off(h->nlist + 1);
       HIPCHECK(hipMemcpy(off.data(), h->d_off.p, sizeof(int64_t) * (h->nlist + 1), hipMemcpyDeviceToHost));

@@ -138,3 +138,58 @@ def test_add_device_large_nlist_segmented_assignment():
         got_c[i] = ix.invlists.get_codes(l).reshape(-1, M)
     np.testing.assert_array_equal(got_l, lo)
     np.testing.assert_array_equal(got_c, co)
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_incremental_adds_in_50k_chunks(shard):
+    """beir's FaissIndex.build adds in 50k chunks (beir/beir/retrieval/search/
+    dense/faiss_index.py:40-42): 8 device and host adds of 50k vectors with
+    random user ids (labels interleave across chunks, so the per-list merge
+    places new entries between old ones), a search after the third chunk (the
+    pending entries are merged into the image then) and list reads at the end.
+    Every list holds exactly the oracle's (list, code) per label, label-sorted,
+    the shard keeps only its lists, and searches equal the oracle."""
+    import torch
+
+    ix, ox = trained_pair(seed=7)
+    lo_l, hi_l = (64, 192) if shard else (0, 256)
+    ix.set_list_range(lo_l, hi_l)
+    rng = np.random.default_rng(3)
+    n, ch = 400_000, 50_000
+    xb = datasets.synthetic_sift_like(n, 64, seed=17, n_centres=500)
+    ids = rng.permutation(10_000_000)[:n].astype(np.int64)
+    xq = datasets.synthetic_sift_like(128, 64, seed=18, n_centres=500)
+    lo, co = ox.encode(xb)
+    keep = (lo >= lo_l) & (lo < hi_l)
+    ix.nprobe = ox.nprobe = 24
+    for c in range(0, n, ch):
+        if (c // ch) % 2 == 0:
+            ix.add_device(torch.from_numpy(xb[c:c + ch]).cuda(), torch.from_numpy(ids[c:c + ch]).cuda())
+        else:
+            ix.add_with_ids(xb[c:c + ch], ids[c:c + ch])
+        assert ix.ntotal == int(keep[:c + ch].sum())
+        if c == 2 * ch:  # a search between adds merges the pending chunks into the image
+            ox2 = O.OracleIVFPQ(64, 256, 16)
+            ox2.set_trained(ix.centroids(), ix.codebook())
+            k3 = keep[:3 * ch]
+            ox2.add_preencoded(lo[:3 * ch][k3], co[:3 * ch][k3], ids[:3 * ch][k3])
+            ox2.nprobe = 24
+            D, I = ix.search(xq, 10)
+            Dr, Ir = ox2.search(xq, 10)
+            np.testing.assert_array_equal(I, Ir)
+            np.testing.assert_array_equal(D, Dr)
+    by_id = {int(i): j for j, i in enumerate(ids)}
+    sizes = ix.invlists.list_sizes()
+    assert sizes[:lo_l].sum() == 0 and sizes[hi_l:].sum() == 0
+    for l, (codes, lids) in enumerate(lists_of(ix)):
+        assert np.all(np.diff(lids) > 0)  # label-sorted
+        j = np.array([by_id[int(i)] for i in lids], np.int64)
+        np.testing.assert_array_equal(lo[j], l)
+        np.testing.assert_array_equal(codes, co[j])
+    ox.add_preencoded(lo[keep], co[keep], ids[keep])
+    for k in (10, 100):
+        D, I = ix.search(xq, k)
+        Dr, Ir = ox.search(xq, k)
+        np.testing.assert_array_equal(I, Ir)
+        np.testing.assert_array_equal(D, Dr)
+    assert ix.error_count() == 0

@@ -75,8 +75,9 @@ def test_c4_rank0_shard_16m_vectors(c4_rank0_shard, k):
     assert sizes[lo:hi].mean() > 1500 and sizes[hi:].sum() == 0
     D, I = ix.search(xq, k)
     Dr, Ir = ox.search(xq, k)
-    assert (I[:, 0] >= 0).all()  # every query has probes that land in the shard
     assert_same(D, I, Dr, Ir)
+    # a query's 32 probes miss the shard's eighth of the lists with probability ~ (7/8)^32
+    assert (I[:, 0] >= 0).mean() > 0.9
     assert ix.error_count() == 0
 
 

@@ -76,7 +76,7 @@ def test_c2_encode_parity_and_result_shape(sift1m):
     slice of the base set; results are sorted, with no duplicate labels."""
     ix, ox, xq = sift1m
     # the first 20k base vectors (the generator draws in blocks of 65536)
-    xb = datasets.synthetic_sift_like(65_536, 128, seed=1234, n_centres=10000)[:20_000]
+    xb = datasets.synthetic_sift_like(65_536, 128, seed=1234, n_centres=200_000)[:20_000]
     lo, co = ox.encode(xb)
     ids0 = np.concatenate([ix.invlists.get_ids(l) for l in range(ix.nlist)])
     lists_all = np.concatenate([np.full(ix.invlists.list_size(l), l) for l in range(ix.nlist)])
