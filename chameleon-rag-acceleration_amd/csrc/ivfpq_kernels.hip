@@ -1566,7 +1566,7 @@ __device__ __forceinline__ int2 fused_plan_prefix(const ListPlan& pl, int nloc, 
     sb += b[u];
   }
   const int ia = wave_incl_scan(sa, lane), ib = wave_incl_scan(sb, lane);
-  if (lane == 63) {
+  if (lane == 63 && wave < 4) {  // (larger workgroups: waves past the first 4 hold no ranks)
     ws[wave] = ia;
     ws[4 + wave] = ib;
   }
@@ -2190,6 +2190,435 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     DIAG(3, __builtin_amdgcn_s_memtime());
     it_no++;
     cur = nxt;
+  }
+}
+
+// ------------------------------------------ pipelined list scan (k <= 16)
+// k_scan_pipe: the list scan of k_scan_lists<M, 4, 1, JB, true> (C2: M = 16,
+// k = 10) restructured so that the LUT build leaves the critical path.  One
+// 768-thread workgroup per CU: 8 scan waves scan item i out of LUT buffer i & 1
+// while 4 loader waves load item i + 1's T1 row and 4 T3 rows (80 KB at M = 16)
+// and write its LUT into the other buffer; one workgroup barrier per item hands
+// the buffers over.  Loader wave 8 also takes the item after next from the work
+// counter and stages its record words in LDS (3 slots: item i scanned, i + 1
+// built, i + 2 fetched), so the scan waves can start item i + 1's code loads
+// before that barrier.  The 8 scan waves split an item's codes (chunk of 64
+// codes per wave, 512 per step); waves w and w + 4 merge their row-packed
+// top-k in LDS at the next item's start and wave w writes the partial list of
+// slot (pair, w), so the merge kernels see the 4 per-wave lists per pair that
+// k_scan_lists writes.  Every candidate key is computed, admitted, queued and
+// ranked exactly as in k_scan_lists (same fp32 order, same (key, position)
+// ranking): results are identical.
+constexpr int kPipeScan = 8, kPipeLoad = 4, kPipeT = 64 * (kPipeScan + kPipeLoad);
+constexpr int kPipeQ = 128;  // candidate queue entries per scan wave (32 per pair)
+
+template <int M, int JB>
+__global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl) {
+  constexpr int G = 4;
+  constexpr int LUTN = M * 256;
+  constexpr int NV = LUTN / 4 / 256;  // float4 rows per loader thread and table
+  constexpr int QG = kPipeQ / G;
+  constexpr int CH = 64 * kPipeScan;  // codes per chunk step of the workgroup
+  static_assert(JB % 2 == 0, "chunks are gathered in pairs");
+  __shared__ __attribute__((aligned(16))) float4 lut[2][LUTN];
+  __shared__ float qd[kPipeScan][kPipeQ];
+  __shared__ int32_t qi[kPipeScan][kPipeQ];
+  __shared__ uint16_t s_ex[2][kFusedPlanLists + 1];
+  __shared__ uint16_t s_ord[kFusedPlanLists];
+  __shared__ uint64_t s_rows[2][4][64];  // waves 4..7's top-k rows, merged by waves 0..3
+  __shared__ int32_t s_rec[3][16];       // record words of the items in flight (item mod 3)
+  __shared__ int32_t s_idx[3];           // their item numbers (-1: none)
+  __shared__ int32_t s_tq[2][G];         // the built item's query bounds (read by the loaders)
+  __shared__ int32_t s_wb[2][G];         // the item's bounds found by its scan waves
+  __shared__ int s_qn[kPipeScan][G];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int k = a.k;
+  const int ip = a.ip;
+  const int nloc = a.list_hi - a.list_lo;
+  const uint64_t lanemask_lt = (1ull << lane) - 1;
+  const float inv_np = 1.0f / (float)a.nprobe;
+  const int2 nn = fused_plan_prefix(pl, nloc, G, s_ex[0], s_ex[1], s_ord, reinterpret_cast<int*>(qi));
+  const int n_items0 = nn.x, n_items = nn.x + nn.y;
+
+  auto unpack = [&](Item<G>& it, int rv) __attribute__((always_inline)) {
+    it.l = __builtin_amdgcn_readlane(rv, 0);
+    const int t = __builtin_amdgcn_readlane(rv, 14);
+    it.cnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - t * G);
+    it.n = __builtin_amdgcn_readlane(rv, 2) - __builtin_amdgcn_readlane(rv, 3);
+    it.beg = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane(rv, 3));
+    it.kind = __builtin_amdgcn_readlane(rv, 13);
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      it.pair[g] = __builtin_amdgcn_readlane(rv, 5 + g);
+      it.d0[g] = __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g));
+    }
+    bool bad = false;
+#pragma unroll
+    for (int g = 0; g < G; g++)
+      bad = bad || (g < it.cnt && (unsigned)it.pair[g] >= (unsigned)(a.nq * a.nprobe));
+    if (bad) {
+      if (lane == 0) atomicAdd(pl.err, 1);
+      it.cnt = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) it.pair[g] = 0;
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
+  };
+  // loader wave 8: take the next item and stage its record words in slot sl
+  auto take = [&](int sl) __attribute__((always_inline)) {
+    int e = 0;
+    if (lane == 0) e = atomicAdd(pl.hdr + 2, 1);
+    e = __builtin_amdgcn_readfirstlane(e);
+    if (e < n_items) {
+      const int rv = fused_record(a, pl, nloc, e, n_items0, s_ex[0], s_ex[1], s_ord, G, lane);
+      if (lane < 16) s_rec[sl][lane] = rv;
+    }
+    if (lane == 0) s_idx[sl] = e < n_items ? e : -1;
+  };
+  // loader waves: item of slot sl -> LUT buffer b (T1 - 2 T3 or -T3, 4 pairs interleaved), its bounds
+  auto build = [&](int sl, int b) __attribute__((always_inline)) {
+    Item<G> it;
+    unpack(it, s_rec[sl][lane & 15]);
+    const int ltid = tid - 64 * kPipeScan;
+    if (ltid < G) {
+      int q = it.q[0];
+#pragma unroll
+      for (int g = 1; g < G; g++) q = ltid == g ? it.q[g] : q;
+      s_tq[b][ltid] = tau_get(pl, q);
+      s_wb[b][ltid] = f2ord(kInf);
+    }
+    const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)it.q[0] * LUTN
+                                                           : a.T1 + (int64_t)it.l * LUTN);
+    float4 b1[NV], b3[NV][G];
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+      const int v = e * 256 + ltid;
+      b1[e] = T1l[v];
+#pragma unroll
+      for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN)[v];
+    }
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+      const int v = e * 256 + ltid;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        float4 o;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          const float x3 = comp(b3[e][g], c);
+          const float lv = ip ? -x3 : comp(b1[e], c) + (-2.0f * x3);
+          setc(o, g, g < it.cnt ? lv : 0.f);
+        }
+        lut[b][4 * v + c] = o;
+      }
+    }
+  };
+
+  // prologue: items 0 and 1 staged, item 0 built
+  if (wave == kPipeScan) {
+    take(0);
+    take(1);
+  }
+  __syncthreads();
+  if (!(wave < kPipeScan) && s_idx[0] >= 0) build(0, 0);
+  __syncthreads();
+
+  // scan-wave state carried across items
+  CodeWords<M> cw[JB];
+  bool have_codes = false;  // cw holds this item's first step (loaded before the barrier)
+  uint64_t prev_rk = kKcNone;
+  int prev_cnt = 0, prev_pair[G];
+  int64_t prev_beg = 0;
+#pragma unroll
+  for (int g = 0; g < G; g++) prev_pair[g] = 0;
+
+  for (int P = 0;; P++) {
+    const int sl = P % 3, b = P & 1;
+    // waves 0..3: the previous item's partial lists (own rows merged with wave w + 4's)
+    if (wave < 4 && prev_cnt > 0) {
+      const uint64_t c = s_rows[b ^ 1][wave][lane];
+      const uint64_t rv = ((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(c >> 32)) << 32) |
+                          (uint32_t)rev16_i((int)(uint32_t)c);
+      uint64_t q = rv < prev_rk ? rv : prev_rk;
+      kc_steps<128, 8>(q, lane);
+      const int rg = lane >> 4, re = lane & 15;
+      int pr = prev_pair[0];
+#pragma unroll
+      for (int g = 1; g < G; g++) pr = rg == g ? prev_pair[g] : pr;
+      if (rg < prev_cnt && re < k) {
+        const int64_t o = ((int64_t)pr * 4 + wave) * k + re;
+        const bool empty = q == kKcNone;
+        pl.partD[o] = empty ? FLT_MAX : kc_key(q);
+        pl.partI[o] = empty ? -1 : prev_beg + (int64_t)(uint32_t)q;
+      }
+    }
+    prev_cnt = 0;
+    if (s_idx[sl] < 0) break;  // workgroup-uniform (LDS, written before the last barrier)
+
+    if (!(wave < kPipeScan)) {
+      // ---------------------------------------------------------------- loaders
+      if (wave == kPipeScan) take((P + 2) % 3);
+      if (s_idx[(P + 1) % 3] >= 0) build((P + 1) % 3, b ^ 1);
+    } else {
+      // ------------------------------------------------------------- scanners
+      Item<G> it;
+      unpack(it, s_rec[sl][lane & 15]);
+      const int n = it.n;
+      const uint8_t* lc = a.codes + it.beg * M;
+      int qix[G];
+      float bound[G];
+      bool loose = false;
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        qix[g] = it.q[g];
+        bound[g] = g < it.cnt ? ord2f(s_tq[b][g]) : -kInf;
+        loose = loose || bound[g] == kInf;
+      }
+      uint64_t rk = kKcNone;  // row g = pair g's sorted top-16
+      uint64_t rtp[G];        // pair g's k-th word (admission threshold)
+      int qn[G];
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        rtp[g] = kKcNone;
+        qn[g] = 0;
+      }
+      auto drain = [&]() __attribute__((always_inline)) {
+        int qmax = 0;
+#pragma unroll
+        for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
+        const int rg = lane >> 4, re = lane & 15;
+        int qr = qn[0];
+#pragma unroll
+        for (int g = 1; g < G; g++) qr = rg == g ? qn[g] : qr;
+        uint64_t thr = rtp[0];
+#pragma unroll
+        for (int g = 1; g < G; g++) thr = rg == g ? rtp[g] : thr;
+        for (int b0 = 0; b0 < qmax; b0 += 16) {
+          const int e = b0 + re;
+          uint64_t c = e < qr ? pack_kc(qd[wave][rg * QG + e], qi[wave][rg * QG + e]) : kKcNone;
+          c = c < thr ? c : kKcNone;
+          if (__builtin_amdgcn_ballot_w64(c != kKcNone) == 0) continue;
+          kc_steps<2, 1>(c, lane);
+          kc_steps<4, 2>(c, lane);
+          kc_steps<8, 4>(c, lane);
+          kc_steps<128, 8>(c, lane);
+          const uint64_t rv = ((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(c >> 32)) << 32) |
+                              (uint32_t)rev16_i((int)(uint32_t)c);
+          uint64_t q = rv < rk ? rv : rk;
+          kc_steps<128, 8>(q, lane);
+          rk = q;
+#pragma unroll
+          for (int g = 0; g < G; g++) rtp[g] = readlane_u64(rk, 16 * g + k - 1);
+          thr = rtp[0];
+#pragma unroll
+          for (int g = 1; g < G; g++) thr = rg == g ? rtp[g] : thr;
+        }
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
+          qn[g] = 0;
+        }
+        loose = false;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          loose = loose || bound[g] == kInf;
+          if (g < it.cnt && rtp[g] != kKcNone && lane == 0) {
+            atomicMin(&s_wb[b][g], f2ord(kc_key(rtp[g])));
+            tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
+          }
+        }
+      };
+
+      for (int sb = 0; sb < n; sb += CH * JB) {
+        if (sb > 0 || !have_codes) {
+#pragma unroll
+          for (int j = 0; j < JB; j++) {
+            const int i = sb + j * CH + wave * 64 + lane;
+            cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
+          }
+        }
+        const int tn = min(JB, (n - sb + CH - 1) / CH);  // chunk steps with codes (wave-uniform)
+        const bool last_sb = sb + CH * JB >= n;
+        float dis[JB][G];
+#pragma unroll
+        for (int jd = 0; jd < JB / 2; jd++) {
+          if (2 * jd < tn) {
+            CodeWords<M> cc[2] = {cw[2 * jd], cw[2 * jd + 1]};
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+              for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(cc[h].w[v]));
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+              for (int g = 0; g < G; g++) dis[2 * jd + h][g] = it.d0[g];
+#pragma unroll
+            for (int m = 0; m < M; m++) {
+#pragma unroll
+              for (int h = 0; h < 2; h++) {
+                const float4 v = lut[b][m * 256 + cc[h].byte(m)];
+#pragma unroll
+                for (int g = 0; g < G; g++) dis[2 * jd + h][g] = dis[2 * jd + h][g] + comp(v, g);
+              }
+            }
+          }
+        }
+        // a query without a bound gets one from this step: the k-th smallest of
+        // the 64 lane minima (k distinct codes) bounds the final k-th key
+        if (loose) {
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            if (bound[g] != kInf) continue;  // wave-uniform
+            float mn = kInf;
+#pragma unroll
+            for (int j = 0; j < JB; j++)
+              if (j < tn && sb + j * CH + wave * 64 + lane < n) mn = fminf(mn, dis[j][g]);
+            const float T = wave_kth_smallest(mn, k, lane);
+            if (T < kInf && lane == 0) {
+              atomicMin(&s_wb[b][g], f2ord(T));
+              tau_lower(pl, qix[g], f2ord(T));
+            }
+          }
+        }
+        loose = false;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[b][g]));
+          loose = loose || bound[g] == kInf;
+        }
+        int t = 0;
+        bool pend = false;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < JB; j++) {
+          if (j < tn) {
+            const bool valid = sb + j * CH + wave * 64 + lane < n;
+#pragma unroll
+            for (int g = 0; g < G; g++) bits |= (uint32_t)(valid && dis[j][g] <= bound[g]) << (j * G + g);
+          }
+        }
+        if (__builtin_amdgcn_ballot_w64(bits != 0) == 0) {
+          t = tn;
+        } else if (!loose) {
+          const int c = __popc(bits);
+          int tot = 0;
+#pragma unroll
+          for (int bb = 0; bb < 5; bb++) tot += __popcll(__builtin_amdgcn_ballot_w64((c >> bb) & 1)) << bb;
+          int qmax = 0;
+#pragma unroll
+          for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
+          if (qmax + tot <= QG) {
+            if (lane == 0)
+#pragma unroll
+              for (int g = 0; g < G; g++) s_qn[wave][g] = qn[g];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < JB; j++) {
+#pragma unroll
+              for (int g = 0; g < G; g++) {
+                if ((bits >> (j * G + g)) & 1u) {
+                  const int q = g * QG + atomicAdd(&s_qn[wave][g], 1);
+                  qd[wave][q] = dis[j][g];
+                  qi[wave][q] = sb + j * CH + wave * 64 + lane;
+                }
+              }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int g = 0; g < G; g++) qn[g] = s_qn[wave][g];
+            t = tn;
+          }
+        }
+        while (t < tn) {
+          int stop = tn;
+          bool want = false;
+          bool go = true;
+#pragma unroll
+          for (int j = 0; j < JB; j++) {
+            if (go && j >= t && j < tn) {
+              const int i = sb + j * CH + wave * 64 + lane;
+              const bool valid = i < n;
+              uint64_t mk[G];
+              int tj = 0;
+#pragma unroll
+              for (int g = 0; g < G; g++) {
+                mk[g] = __builtin_amdgcn_ballot_w64(valid && dis[j][g] <= bound[g]);
+                tj += __popcll(mk[g]);
+              }
+              bool full = false;
+#pragma unroll
+              for (int g = 0; g < G; g++) full = full || qn[g] + __popcll(mk[g]) > QG;
+              if (tj > 0) {
+                if (full) {
+                  stop = j;
+                  want = true;
+                  go = false;
+                } else {
+#pragma unroll
+                  for (int g = 0; g < G; g++) {
+                    if ((mk[g] >> lane) & 1) {
+                      const int q = g * QG + qn[g] + __popcll(mk[g] & lanemask_lt);
+                      qd[wave][q] = dis[j][g];
+                      qi[wave][q] = i;
+                    }
+                    qn[g] += __popcll(mk[g]);
+                  }
+                  if (loose) {
+                    stop = j + 1;
+                    want = true;
+                    go = false;
+                  }
+                }
+              }
+            }
+          }
+          if (stop >= tn) {
+            pend = want;
+            break;
+          }
+          drain();
+          t = stop;
+        }
+        bool queued = false;
+#pragma unroll
+        for (int g = 0; g < G; g++) queued = queued || qn[g] > 0;
+        if (pend || (last_sb && queued)) drain();
+      }
+      // the next item's first codes, in flight across the barrier (its record was
+      // staged a phase ago)
+      have_codes = false;
+      const int ns = (P + 1) % 3;
+      if (s_idx[ns] >= 0) {
+        const int w2 = s_rec[ns][2], w3 = s_rec[ns][3], w4 = s_rec[ns][4];
+        const int n2 = w2 - w3;
+        const uint8_t* lc2 = a.codes + (int64_t)(((uint64_t)(uint32_t)w4 << 32) | (uint32_t)w3) * M;
+#pragma unroll
+        for (int j = 0; j < JB; j++) {
+          const int i = j * CH + wave * 64 + lane;
+          cw[j].load(lc2 + (int64_t)(i < n2 ? i : 0) * M);
+        }
+        have_codes = true;
+      }
+      if (wave >= 4) {
+        s_rows[b][wave - 4][lane] = rk;
+      } else {
+        prev_rk = rk;
+        prev_cnt = it.cnt;
+        prev_beg = it.beg;
+#pragma unroll
+        for (int g = 0; g < G; g++) prev_pair[g] = it.pair[g];
+      }
+    }
+    __syncthreads();  // item P scanned, item P + 1 built, item P + 2 staged
   }
 }
 
@@ -2953,6 +3382,22 @@ int scan_lists_grid(int M, int k) {
   return std::max(8, (per_cu * cus + 7) / 8 * 8);
 }
 
+// the pipelined scan (k_scan_pipe) serves k <= 16 at M <= 16 with fused planning;
+// -DSCAN_PIPE=0 builds the A/B variant that runs k_scan_lists there instead
+#ifndef SCAN_PIPE
+#define SCAN_PIPE 1
+#endif
+
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    cus = n;
+  }
+  return cus;
+}
+
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
@@ -2960,6 +3405,14 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   // 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
   constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : 2;
   if (ev) (void)hipEventRecord(ev[0], s);
+  if constexpr (G == 4 && R == 1 && M <= 16 && SCAN_PIPE) {
+    if (a.k <= 16 && pl.fused) {  // one workgroup per CU
+      hipLaunchKernelGGL((k_scan_pipe<M, 4>), dim3((unsigned)device_cus()), dim3(kPipeT), 0, s, a, pl);
+      if (ev) (void)hipEventRecord(ev[1], s);
+      hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
+      return;
+    }
+  }
   if constexpr (G == 4 && R == 1) {
     if (a.k <= 16) {  // r03 A/B at C2: 115.1 vs 125.7 us
       hipLaunchKernelGGL((k_scan_lists<M, G, R, JB, true>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
