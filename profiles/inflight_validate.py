@@ -63,7 +63,9 @@ def main():
             out["batches_per_k"] += rounds * nb
     out["index_check_errors"] = ix.error_count()
     out["seconds"] = time.time() - t0
-    out["lib"] = os.path.relpath(faiss._lib.LIB_PATH, R) if hasattr(faiss, "_lib") else None
+    from faiss_amd import _lib
+
+    out["lib"] = os.path.relpath(_lib.LIB_PATH, R)
     print(json.dumps(out), flush=True)
 
 
