@@ -1671,6 +1671,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table
   __shared__ __attribute__((aligned(16))) V lut[LUTN];
   constexpr int QG = QCAP / G;  // queue entries per wave and pair
+  static_assert(QG >= 64, "a chunk's candidates must fit an empty queue");
   __shared__ float qd[4][QCAP];    // [wave][g][QG]
   __shared__ int32_t qi[4][QCAP];  // positions in the list
   __shared__ int s_next;
@@ -2210,7 +2211,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 // ranked exactly as in k_scan_lists (same fp32 order, same (key, position)
 // ranking): results are identical.
 constexpr int kPipeScan = 8, kPipeLoad = 4, kPipeT = 64 * (kPipeScan + kPipeLoad);
-constexpr int kPipeQ = 128;  // candidate queue entries per scan wave (32 per pair)
+// candidate queue entries per scan wave: >= 64 per pair, so that a drained queue
+// always takes a whole 64-code chunk (the admission loop's progress guarantee)
+constexpr int kPipeQ = 256;
 
 template <int M, int JB>
 __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl) {
@@ -2218,6 +2221,7 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
   constexpr int LUTN = M * 256;
   constexpr int NV = LUTN / 4 / 256;  // float4 rows per loader thread and table
   constexpr int QG = kPipeQ / G;
+  static_assert(QG >= 64, "a chunk's candidates must fit an empty queue");
   constexpr int CH = 64 * kPipeScan;  // codes per chunk step of the workgroup
   static_assert(JB % 2 == 0, "chunks are gathered in pairs");
   __shared__ __attribute__((aligned(16))) float4 lut[2][LUTN];
@@ -2294,27 +2298,33 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
     }
     const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)it.q[0] * LUTN
                                                            : a.T1 + (int64_t)it.l * LUTN);
-    float4 b1[NV], b3[NV][G];
+    // rows in groups of NVG (40 staging VGPRs at NVG = 2): the loaders have a whole
+    // scan phase for the round trips, the registers are the scarcer resource
+    constexpr int NVG = NV < 2 ? NV : 2;
 #pragma unroll
-    for (int e = 0; e < NV; e++) {
-      const int v = e * 256 + ltid;
-      b1[e] = T1l[v];
+    for (int e0 = 0; e0 < NV; e0 += NVG) {
+      float4 b1[NVG], b3[NVG][G];
 #pragma unroll
-      for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN)[v];
-    }
+      for (int e = 0; e < NVG; e++) {
+        const int v = (e0 + e) * 256 + ltid;
+        b1[e] = T1l[v];
 #pragma unroll
-    for (int e = 0; e < NV; e++) {
-      const int v = e * 256 + ltid;
+        for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN)[v];
+      }
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
-        float4 o;
+      for (int e = 0; e < NVG; e++) {
+        const int v = (e0 + e) * 256 + ltid;
 #pragma unroll
-        for (int g = 0; g < G; g++) {
-          const float x3 = comp(b3[e][g], c);
-          const float lv = ip ? -x3 : comp(b1[e], c) + (-2.0f * x3);
-          setc(o, g, g < it.cnt ? lv : 0.f);
+        for (int c = 0; c < 4; c++) {
+          float4 o;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            const float x3 = comp(b3[e][g], c);
+            const float lv = ip ? -x3 : comp(b1[e], c) + (-2.0f * x3);
+            setc(o, g, g < it.cnt ? lv : 0.f);
+          }
+          lut[b][4 * v + c] = o;
         }
-        lut[b][4 * v + c] = o;
       }
     }
   };
@@ -3407,7 +3417,7 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   if (ev) (void)hipEventRecord(ev[0], s);
   if constexpr (G == 4 && R == 1 && M <= 16 && SCAN_PIPE) {
     if (a.k <= 16 && pl.fused) {  // one workgroup per CU
-      hipLaunchKernelGGL((k_scan_pipe<M, 4>), dim3((unsigned)device_cus()), dim3(kPipeT), 0, s, a, pl);
+      hipLaunchKernelGGL((k_scan_pipe<M, 2>), dim3((unsigned)device_cus()), dim3(kPipeT), 0, s, a, pl);
       if (ev) (void)hipEventRecord(ev[1], s);
       hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
       return;

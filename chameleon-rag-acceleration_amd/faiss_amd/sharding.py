@@ -58,7 +58,10 @@ def exchange_partials(Dp, Ip, world, group=None):
 
     Dp, Ip: [world * B, k] partial top-k over this rank's lists for the global
     batch.  Returns (Ds, Is) of shape [world, B, k]: entry s holds rank s's
-    partial for this rank's query slice.
+    partial for this rank's query slice.  One ``all_to_all_single`` per array:
+    row block j of the input (slice j of the batch) goes to rank j, and the
+    output's row block s comes from rank s (RCCL over xGMI on GPUs; gloo runs
+    the same call on CPU tensors in the multi-process tests).
     """
     import torch
     import torch.distributed as dist
@@ -71,34 +74,19 @@ def exchange_partials(Dp, Ip, world, group=None):
         Ds[0].copy_(Dp)
         Is[0].copy_(Ip)
         return Ds, Is
-    if dist.get_backend(group) == "gloo":  # gloo has no all_to_all: gather then slice
-        rank = dist.get_rank(group)
-        gD = [torch.empty_like(Dp) for _ in range(world)]
-        gI = [torch.empty_like(Ip) for _ in range(world)]
-        dist.all_gather(gD, Dp.contiguous(), group=group)
-        dist.all_gather(gI, Ip.contiguous(), group=group)
-        for s in range(world):
-            Ds[s].copy_(gD[s][rank * B:(rank + 1) * B])
-            Is[s].copy_(gI[s][rank * B:(rank + 1) * B])
-        return Ds, Is
     dist.all_to_all_single(Ds.view(world * B, k), Dp.contiguous(), group=group)
     dist.all_to_all_single(Is.view(world * B, k), Ip.contiguous(), group=group)
     return Ds, Is
 
 
 def all_gather_probes(Dq, Iq, world, group=None):
-    """All-gather of the per-slice coarse results: [B, nprobe] -> [world * B, nprobe]."""
+    """All-gather of the per-slice coarse results: [B, nprobe] -> [world * B, nprobe]
+    (slice r from rank r), one ``all_gather_into_tensor`` per array."""
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return Dq, Iq
-    if dist.get_backend(group) == "gloo":
-        gD = [torch.empty_like(Dq) for _ in range(world)]
-        gI = [torch.empty_like(Iq) for _ in range(world)]
-        dist.all_gather(gD, Dq.contiguous(), group=group)
-        dist.all_gather(gI, Iq.contiguous(), group=group)
-        return torch.cat(gD), torch.cat(gI)
     outD = torch.empty((world * Dq.shape[0], Dq.shape[1]), dtype=Dq.dtype, device=Dq.device)
     outI = torch.empty((world * Iq.shape[0], Iq.shape[1]), dtype=Iq.dtype, device=Iq.device)
     dist.all_gather_into_tensor(outD, Dq.contiguous(), group=group)

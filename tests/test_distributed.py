@@ -1,7 +1,7 @@
 """Multi-process list-range sharding on CPU (gloo, world_size 2).
 
 Each rank holds only its inverted-list range; the partial results of the
-global batch are exchanged (all_to_all; all_gather under gloo) and merged by
+global batch are exchanged (all_to_all_single; gloo runs the same collectives) and merged by
 (distance, label).  The sharded result must equal the unsharded oracle search.
 """
 import os
@@ -113,3 +113,56 @@ def test_sharded_search_equals_unsharded(tmp_path, golden_dir, case, slice_coars
     z = np.load(golden)
     np.testing.assert_array_equal(r["I"], z["or_I"])
     np.testing.assert_array_equal(r["D"], z["or_D"])
+
+
+def _collective_worker(rank, world, port, out):
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "chameleon-rag-acceleration_amd"))
+    import torch
+    import torch.distributed as dist
+
+    from faiss_amd.sharding import all_gather_probes, exchange_partials
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, k, np_ = 5, 3, 4
+    g = torch.Generator().manual_seed(rank)
+    Dp = torch.rand((world * B, k), generator=g)
+    Ip = torch.randint(0, 1 << 40, (world * B, k), generator=g)
+    Ds, Is = exchange_partials(Dp, Ip, world)
+    # reference: gather every rank's whole partial array, then take this rank's slice of each
+    gD = [torch.empty_like(Dp) for _ in range(world)]
+    gI = [torch.empty_like(Ip) for _ in range(world)]
+    dist.all_gather(gD, Dp)
+    dist.all_gather(gI, Ip)
+    ok = all(torch.equal(Ds[s], gD[s][rank * B:(rank + 1) * B]) and torch.equal(Is[s], gI[s][rank * B:(rank + 1) * B])
+             for s in range(world))
+    Dq = torch.rand((B, np_), generator=g)
+    Iq = torch.randint(0, 1024, (B, np_), generator=g)
+    aD, aI = all_gather_probes(Dq, Iq, world)
+    hD = [torch.empty_like(Dq) for _ in range(world)]
+    hI = [torch.empty_like(Iq) for _ in range(world)]
+    dist.all_gather(hD, Dq)
+    dist.all_gather(hI, Iq)
+    ok = ok and torch.equal(aD, torch.cat(hD)) and torch.equal(aI, torch.cat(hI))
+    flags = [torch.zeros(1) for _ in range(world)]
+    dist.all_gather(flags, torch.tensor([1.0 if ok else 0.0]))
+    if rank == 0:
+        np.save(out, np.array([float(f) for f in flags]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_exchange_collectives_slicing(tmp_path, world):
+    """The collectives bench.py's shard step runs over RCCL (all_to_all_single of
+    the partials, all_gather_into_tensor of the probes), executed here under gloo:
+    rank r receives slice r of every rank's partials in rank order, and the
+    probes of slice s come from rank s -- the layout of a gather-then-slice
+    reference."""
+    out = str(tmp_path / "ok.npy")
+    mp.spawn(_collective_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert np.load(out).tolist() == [1.0] * world
