@@ -1448,6 +1448,25 @@ __device__ __forceinline__ void kc_row16_merge(PackedTopK<1>& tk, uint64_t c, in
 }
 
 
+// Row-packed top-k (ROWK): pair g's sorted k <= 16 best words live in lanes
+// 16 g .. 16 g + 15 of one 64-bit register.  Insert word v into row g (the
+// row's last word drops out): lanes past v's rank take their left neighbour
+// (DPP row_shr:1 stays inside the row), the rank lane takes v.
+__device__ __forceinline__ uint64_t row_insert(uint64_t rk, int g, uint64_t v, int lane) {
+  const bool inrow = (lane >> 4) == g;
+  const int pos = __popcll(__builtin_amdgcn_ballot_w64(inrow && rk < v));  // words of row g below v
+  const int re = lane & 15;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)rk, (int)(uint32_t)rk, 0x111, 0xf, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(rk >> 32), (int)(uint32_t)(rk >> 32), 0x111, 0xf, 0xf, false);
+  const uint64_t left = ((uint64_t)hi << 32) | lo;
+  const uint64_t nv = re > pos ? left : (re == pos ? v : rk);
+  return inrow ? nv : rk;
+}
+// candidates of one super-batch that go straight into the rows (no queue, no
+// sorting network) when there are at most this many in the wave
+constexpr int kDirectInsert = 24;
+
 template <int G>
 struct LutVec;
 template <>
@@ -2069,7 +2088,40 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         int qmax = 0;
 #pragma unroll
         for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
-        if (qmax + tot <= QG) {
+        if (ROWK && tot <= kDirectInsert) {
+          // few candidates: each one goes straight into its pair's row (register
+          // DPP shift), in (chunk, pair, lane) order -- the top-k is a set function
+          // of the candidates, so the order does not change the rows
+          bool ins = false;
+#pragma unroll
+          for (int j = 0; j < JB; j++) {
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              uint64_t m = __builtin_amdgcn_ballot_w64((bits >> (j * G + g)) & 1u);
+              while (m) {
+                const int src = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint64_t w = pack_kc(readlane_f(dis[j][g], src), sb + j * 256 + wave * 64 + src);
+                if (w < rtp[g]) {
+                  rk = row_insert(rk, g, w, lane);
+                  rtp[g] = readlane_u64(rk, 16 * g + k - 1);
+                  ins = true;
+                }
+              }
+            }
+          }
+          if (ins) {
+#pragma unroll
+            for (int g = 0; g < G; g++) {
+              bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
+              if (g < it.cnt && rtp[g] != kKcNone && lane == 0) {
+                atomicMin(&s_wb[g], f2ord(kc_key(rtp[g])));
+                tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
+              }
+            }
+          }
+          t = tn;
+        } else if (qmax + tot <= QG) {
           if (lane == 0)
 #pragma unroll
             for (int g = 0; g < G; g++) s_qn[wave][g] = qn[g];
@@ -2349,6 +2401,7 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
 
   for (int P = 0;; P++) {
     const int sl = P % 3, b = P & 1;
+    if (wave == 0) PDIAG(0, __builtin_amdgcn_s_memtime());
     // waves 0..3: the previous item's partial lists (own rows merged with wave w + 4's)
     if (wave < 4 && prev_cnt > 0) {
       const uint64_t c = s_rows[b ^ 1][wave][lane];
@@ -2373,13 +2426,19 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
     if (!(wave < kPipeScan)) {
       // ---------------------------------------------------------------- loaders
       if (wave == kPipeScan) take((P + 2) % 3);
+      if (wave == kPipeScan) PDIAG(1, __builtin_amdgcn_s_memtime());
       if (s_idx[(P + 1) % 3] >= 0) build((P + 1) % 3, b ^ 1);
+      PDIAG_WAIT();
+      if (wave == kPipeScan) PDIAG(2, __builtin_amdgcn_s_memtime());
+      if (wave == kPipeScan + 1) PDIAG(3, __builtin_amdgcn_s_memtime());
     } else {
       // ------------------------------------------------------------- scanners
       Item<G> it;
       unpack(it, s_rec[sl][lane & 15]);
       const int n = it.n;
       const uint8_t* lc = a.codes + it.beg * M;
+      if (wave == 0) PDIAG(13, __builtin_amdgcn_s_memtime());
+      if (wave == 0) PDIAG(12, (uint64_t)n | ((uint64_t)it.cnt << 32) | ((uint64_t)it.kind << 40));
       int qix[G];
       float bound[G];
       bool loose = false;
@@ -2522,7 +2581,37 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
           int qmax = 0;
 #pragma unroll
           for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
-          if (qmax + tot <= QG) {
+          if (tot <= kDirectInsert) {  // few candidates: straight into the rows (as k_scan_lists)
+            bool ins = false;
+#pragma unroll
+            for (int j = 0; j < JB; j++) {
+#pragma unroll
+              for (int g = 0; g < G; g++) {
+                uint64_t m = __builtin_amdgcn_ballot_w64((bits >> (j * G + g)) & 1u);
+                while (m) {
+                  const int src = __builtin_ctzll(m);
+                  m &= m - 1;
+                  const uint64_t w = pack_kc(readlane_f(dis[j][g], src), sb + j * CH + wave * 64 + src);
+                  if (w < rtp[g]) {
+                    rk = row_insert(rk, g, w, lane);
+                    rtp[g] = readlane_u64(rk, 16 * g + k - 1);
+                    ins = true;
+                  }
+                }
+              }
+            }
+            if (ins) {
+#pragma unroll
+              for (int g = 0; g < G; g++) {
+                bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
+                if (g < it.cnt && rtp[g] != kKcNone && lane == 0) {
+                  atomicMin(&s_wb[b][g], f2ord(kc_key(rtp[g])));
+                  tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
+                }
+              }
+            }
+            t = tn;
+          } else if (qmax + tot <= QG) {
             if (lane == 0)
 #pragma unroll
               for (int g = 0; g < G; g++) s_qn[wave][g] = qn[g];
@@ -2618,6 +2707,7 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
         }
         have_codes = true;
       }
+      PDIAG(4 + wave, __builtin_amdgcn_s_memtime());
       if (wave >= 4) {
         s_rows[b][wave - 4][lane] = rk;
       } else {
@@ -3468,7 +3558,7 @@ void launch_merge_topk(int S, int64_t n, int k, const float* Din, const int64_t*
 
 }  // namespace chivf
 
-#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS)
+#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS) || defined(DIAG_PSTAMPS)
 extern "C" int ivfpq_diag_stamps(void* out, size_t bytes) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(chivf::g_diag), bytes) != hipSuccess) return -1;
   static uint64_t zeros[chivf::kDiagWG * chivf::kDiagItems * chivf::kDiagSlots];
