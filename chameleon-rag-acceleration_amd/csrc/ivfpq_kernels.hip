@@ -1448,24 +1448,23 @@ __device__ __forceinline__ void kc_row16_merge(PackedTopK<1>& tk, uint64_t c, in
 }
 
 
-// Row-packed top-k (ROWK): pair g's sorted k <= 16 best words live in lanes
-// 16 g .. 16 g + 15 of one 64-bit register.  Insert word v into row g (the
-// row's last word drops out): lanes past v's rank take their left neighbour
-// (DPP row_shr:1 stays inside the row), the rank lane takes v.
-__device__ __forceinline__ uint64_t row_insert(uint64_t rk, int g, uint64_t v, int lane) {
-  const bool inrow = (lane >> 4) == g;
-  const int pos = __popcll(__builtin_amdgcn_ballot_w64(inrow && rk < v));  // words of row g below v
-  const int re = lane & 15;
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)rk, (int)(uint32_t)rk, 0x111, 0xf, 0xf, false);
-  const uint32_t hi =
-      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(rk >> 32), (int)(uint32_t)(rk >> 32), 0x111, 0xf, 0xf, false);
-  const uint64_t left = ((uint64_t)hi << 32) | lo;
-  const uint64_t nv = re > pos ? left : (re == pos ? v : rk);
-  return inrow ? nv : rk;
+// inclusive prefix sum over the wave on the VALU: 16-lane row scans by DPP
+// row shifts (zero fill), then the row totals added by readlane
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_shr_z(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
 }
-// candidates of one super-batch that go straight into the rows (no queue, no
-// sorting network) when there are at most this many in the wave
-constexpr int kDirectInsert = 24;
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+  uint32_t s = v + dpp_shr_z<0x111>(v) + dpp_shr_z<0x112>(v) + dpp_shr_z<0x113>(v);  // row_shr:1..3
+  s += dpp_shr_z<0x114>(s);                                                          // row_shr:4
+  s += dpp_shr_z<0x118>(s);                                                          // row_shr:8
+  const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)s, 15);
+  const uint32_t t1 = (uint32_t)__builtin_amdgcn_readlane((int)s, 31);
+  const uint32_t t2 = (uint32_t)__builtin_amdgcn_readlane((int)s, 47);
+  const int row = lane >> 4;
+  return s + (row == 0 ? 0u : row == 1 ? t0 : row == 2 ? t0 + t1 : t0 + t1 + t2);
+}
+
 
 template <int G>
 struct LutVec;
@@ -1695,7 +1694,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   __shared__ int32_t qi[4][QCAP];  // positions in the list
   __shared__ int s_next;
   __shared__ int32_t s_wb[G];  // the item's per-query bounds found by its waves (ordered ints)
-  __shared__ int s_qn[4][G];   // queue fills of the slot-counter admission
   // fused planning (pl.fused): the item prefix of every list in scheduling order
   __shared__ uint16_t s_ex[2][kFusedPlanLists + 1];
   __shared__ uint16_t s_ord[kFusedPlanLists];
@@ -2088,62 +2086,39 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
         int qmax = 0;
 #pragma unroll
         for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
-        if (ROWK && tot <= kDirectInsert) {
-          // few candidates: each one goes straight into its pair's row (register
-          // DPP shift), in (chunk, pair, lane) order -- the top-k is a set function
-          // of the candidates, so the order does not change the rows
-          bool ins = false;
+        if (qmax + tot <= QG) {
+          // queue slots from one prefix sum over the wave of the lanes' per-pair
+          // counts, packed 32 / G bits per pair (each pair's total <= tot <= QG fits
+          // its field, so fields never carry into each other): no LDS atomics
+          constexpr int FB = 32 / G;
+          uint32_t cp = 0;
 #pragma unroll
-          for (int j = 0; j < JB; j++) {
+          for (int g = 0; g < G; g++) {
+            uint32_t cg = 0;
 #pragma unroll
-            for (int g = 0; g < G; g++) {
-              uint64_t m = __builtin_amdgcn_ballot_w64((bits >> (j * G + g)) & 1u);
-              while (m) {
-                const int src = __builtin_ctzll(m);
-                m &= m - 1;
-                const uint64_t w = pack_kc(readlane_f(dis[j][g], src), sb + j * 256 + wave * 64 + src);
-                if (w < rtp[g]) {
-                  rk = row_insert(rk, g, w, lane);
-                  rtp[g] = readlane_u64(rk, 16 * g + k - 1);
-                  ins = true;
-                }
-              }
-            }
+            for (int j = 0; j < JB; j++) cg += (bits >> (j * G + g)) & 1u;
+            cp |= cg << (FB * g);
           }
-          if (ins) {
+          const uint32_t incl = wave_incl_scan_u32(cp, lane);
+          const uint32_t totp = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+          const uint32_t at = incl - cp;
+          constexpr uint32_t FM = FB >= 32 ? 0xFFFFFFFFu : (1u << FB) - 1;
+          int off[G];
 #pragma unroll
-            for (int g = 0; g < G; g++) {
-              bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
-              if (g < it.cnt && rtp[g] != kKcNone && lane == 0) {
-                atomicMin(&s_wb[g], f2ord(kc_key(rtp[g])));
-                tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
-              }
-            }
-          }
-          t = tn;
-        } else if (qmax + tot <= QG) {
-          if (lane == 0)
-#pragma unroll
-            for (int g = 0; g < G; g++) s_qn[wave][g] = qn[g];
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          for (int g = 0; g < G; g++) off[g] = g * QG + qn[g] + (int)((at >> (FB * g)) & FM);
 #pragma unroll
           for (int j = 0; j < JB; j++) {
 #pragma unroll
             for (int g = 0; g < G; g++) {
               if ((bits >> (j * G + g)) & 1u) {
-                const int sl = g * QG + atomicAdd(&s_qn[wave][g], 1);
-                qd[wave][sl] = dis[j][g];
-                qi[wave][sl] = sb + j * 256 + wave * 64 + lane;
+                qd[wave][off[g]] = dis[j][g];
+                qi[wave][off[g]] = sb + j * 256 + wave * 64 + lane;
+                off[g]++;
               }
             }
           }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-          for (int g = 0; g < G; g++) qn[g] = s_qn[wave][g];
+          for (int g = 0; g < G; g++) qn[g] += (int)((totp >> (FB * g)) & FM);
           DIAG_ONLY(d_push += tot;)
           t = tn;
         }
@@ -2286,7 +2261,6 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
   __shared__ int32_t s_idx[3];           // their item numbers (-1: none)
   __shared__ int32_t s_tq[2][G];         // the built item's query bounds (read by the loaders)
   __shared__ int32_t s_wb[2][G];         // the item's bounds found by its scan waves
-  __shared__ int s_qn[kPipeScan][G];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -2581,59 +2555,34 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
           int qmax = 0;
 #pragma unroll
           for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
-          if (tot <= kDirectInsert) {  // few candidates: straight into the rows (as k_scan_lists)
-            bool ins = false;
+          if (qmax + tot <= QG) {  // slots from a packed per-pair prefix sum (as k_scan_lists)
+            uint32_t cp = 0;
 #pragma unroll
-            for (int j = 0; j < JB; j++) {
+            for (int g = 0; g < G; g++) {
+              uint32_t cg = 0;
 #pragma unroll
-              for (int g = 0; g < G; g++) {
-                uint64_t m = __builtin_amdgcn_ballot_w64((bits >> (j * G + g)) & 1u);
-                while (m) {
-                  const int src = __builtin_ctzll(m);
-                  m &= m - 1;
-                  const uint64_t w = pack_kc(readlane_f(dis[j][g], src), sb + j * CH + wave * 64 + src);
-                  if (w < rtp[g]) {
-                    rk = row_insert(rk, g, w, lane);
-                    rtp[g] = readlane_u64(rk, 16 * g + k - 1);
-                    ins = true;
-                  }
-                }
-              }
+              for (int j = 0; j < JB; j++) cg += (bits >> (j * G + g)) & 1u;
+              cp |= cg << (8 * g);
             }
-            if (ins) {
+            const uint32_t incl = wave_incl_scan_u32(cp, lane);
+            const uint32_t totp = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            const uint32_t at = incl - cp;
+            int off[G];
 #pragma unroll
-              for (int g = 0; g < G; g++) {
-                bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
-                if (g < it.cnt && rtp[g] != kKcNone && lane == 0) {
-                  atomicMin(&s_wb[b][g], f2ord(kc_key(rtp[g])));
-                  tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
-                }
-              }
-            }
-            t = tn;
-          } else if (qmax + tot <= QG) {
-            if (lane == 0)
-#pragma unroll
-              for (int g = 0; g < G; g++) s_qn[wave][g] = qn[g];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int g = 0; g < G; g++) off[g] = g * QG + qn[g] + (int)((at >> (8 * g)) & 0xffu);
 #pragma unroll
             for (int j = 0; j < JB; j++) {
 #pragma unroll
               for (int g = 0; g < G; g++) {
                 if ((bits >> (j * G + g)) & 1u) {
-                  const int q = g * QG + atomicAdd(&s_qn[wave][g], 1);
-                  qd[wave][q] = dis[j][g];
-                  qi[wave][q] = sb + j * CH + wave * 64 + lane;
+                  qd[wave][off[g]] = dis[j][g];
+                  qi[wave][off[g]] = sb + j * CH + wave * 64 + lane;
+                  off[g]++;
                 }
               }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-            for (int g = 0; g < G; g++) qn[g] = s_qn[wave][g];
+            for (int g = 0; g < G; g++) qn[g] += (int)((totp >> (8 * g)) & 0xffu);
             t = tn;
           }
         }
