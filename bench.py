@@ -85,7 +85,7 @@ def parse():
     p.add_argument("--event-every", type=int, default=5,
                    help="record the list-scan HIP events on every N-th timed step")
     p.add_argument("--no-recall", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r03b_scan_pmc.json"),
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r04_scan_pmc.json"),
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
@@ -354,13 +354,16 @@ def main():
     config_key = (f"nb{args.nb}-d{args.d}-IVF{args.nlist}-PQ{args.M}-np{args.nprobe}-k{k}-B{B}-w{world}-{args.mode}"
                   f"-c{args.centres}")
     sha = lib_sha256()
+    from faiss_amd import _lib
+
+    ksha = _lib.kernel_source_sha256()
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
             if pm.get("config_key") != config_key:
                 traffic_src = "counter file is for another config"
-            elif pm.get("lib_sha256") != sha:
-                traffic_src = "counter file is stale (measured on another build of libivfpq.so)"
+            elif pm.get("kernel_src_sha256") != ksha and pm.get("lib_sha256") != sha:
+                traffic_src = "counter file is stale (measured on another build of the kernels)"
             else:
                 traffic = pm.get("hbm_bytes_per_launch")
                 traffic_src = os.path.relpath(args.pmc_json, REPO)
@@ -401,6 +404,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "lib_sha256": sha,
+                "kernel_src_sha256": ksha,
                 "kernel": kernel,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": avg_launch_ms,

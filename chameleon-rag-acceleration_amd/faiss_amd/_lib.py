@@ -83,6 +83,19 @@ SIGNATURES = {
 }
 
 
+def kernel_source_sha256() -> str:
+    """sha256 of what the GPU kernels are compiled from (the kernel source, its
+    headers, the Makefile's flags): the key under which counter measurements of
+    the kernels stay valid across builds that change host code only."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("ivfpq_kernels.hip", "ivfpq_kernels.h", "ivfpq_diag.h", "Makefile"):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read() + b"\0")
+    return h.hexdigest()
+
+
 def build(force: bool = False) -> str:
     """Compile libivfpq.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
     srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h"))]

@@ -3,7 +3,8 @@
 FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads on gfx950 (doubled here);
 WRITE_SIZE is taken as is.  The FETCH_SIZE unit is checked against TCC_EA0_RDREQ_sum x 64 B
 rather than assumed.  Usage: make_pmc_json.py <pmc dir> <config_key> <out.json> [libivfpq.so]
-The library's sha256 is recorded: bench.py uses the bytes only for the same build."""
+The library's sha256 and the kernel sources' sha256 (faiss_amd._lib.kernel_source_sha256)
+are recorded: bench.py uses the bytes only for the same kernel build."""
 import collections
 import csv
 import glob
@@ -30,6 +31,11 @@ def main(d, key, out, lib=None):
         import hashlib
 
         res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "chameleon-rag-acceleration_amd"))
+    from faiss_amd import _lib
+
+    res["kernel_src_sha256"] = _lib.kernel_source_sha256()
     for k in kernels:
         f = mean.get((k, "FETCH_SIZE"))
         w = mean.get((k, "WRITE_SIZE"))
@@ -43,7 +49,7 @@ def main(d, key, out, lib=None):
         if f is not None and w is not None:
             ent["hbm_bytes_per_launch"] = 2.0 * f * unit + w * unit
         res["kernels"][k] = ent
-    lists = [k for k in kernels if k.startswith("k_scan_lists")]
+    lists = [k for k in kernels if k.startswith(("k_scan_pipe", "k_scan_lists"))]
     topk = [k for k in kernels if k.startswith("k_scan_topk") and "true" not in k]
     main_k = (lists or topk or [None])[0]
     res["kernel"] = main_k
