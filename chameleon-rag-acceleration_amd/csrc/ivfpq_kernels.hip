@@ -28,7 +28,8 @@
 //    lists of its probes, labels looked up for survivors only.
 // Every fp32 operation follows the oracle's order (oracle/ivfpq_oracle.c,
 // Faiss 1.7.1 AVX order); the library is compiled with -ffp-contract=off and
-// the only FMAs are the explicit fmaf() of the coarse inner product.
+// the only FMAs are the explicit fmaf() of the coarse inner product and the
+// LUT's T1 + (-2) T3 (exact product, so one rounding either way).
 #include <float.h>
 #include <stdint.h>
 
@@ -1822,7 +1823,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       const int i = j * 256 + wave * 64 + lane;
       cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);  // clamped: branch-free loads
     }
-    // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved; entries of absent pairs are 0
+    // LUT = T1 - 2 T3 (L2) or -T3 (IP), G interleaved
 #pragma unroll
     for (int u = 0; u < NG; u++) {
       if (u + 1 < NG) fetch(u + 1, (u + 1) & 1);
@@ -1835,8 +1836,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
           for (int g = 0; g < G; g++) {
             const float x3 = comp(b3[u & 1][e][g], c);
-            const float lv = ip ? -x3 : comp(b1[u & 1][e], c) + (-2.0f * x3);
-            setc(o, g, g < it.cnt ? lv : 0.f);
+            // T1 + (-2) T3 as one fma: -2 T3 is exact, so this rounds once like the
+            // oracle's add of the product; entries of absent pairs are never admitted
+            const float lv = ip ? -x3 : __builtin_fmaf(x3, -2.0f, comp(b1[u & 1][e], c));
+            setc(o, g, lv);
           }
           lut[4 * v + c] = o;
         }
@@ -2346,8 +2349,8 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
 #pragma unroll
           for (int g = 0; g < G; g++) {
             const float x3 = comp(b3[e][g], c);
-            const float lv = ip ? -x3 : comp(b1[e], c) + (-2.0f * x3);
-            setc(o, g, g < it.cnt ? lv : 0.f);
+            const float lv = ip ? -x3 : __builtin_fmaf(x3, -2.0f, comp(b1[e], c));  // (as k_scan_lists)
+            setc(o, g, lv);
           }
           lut[b][4 * v + c] = o;
         }
