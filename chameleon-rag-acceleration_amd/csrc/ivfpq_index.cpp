@@ -158,6 +158,12 @@ constexpr size_t kPartialBytes = size_t(2048) << 20;  // bound for a chunk's per
 // C2, nlist 1024: segmented 22.5 + 8.5 us + a separate T3 launch 13.0 us vs key
 // matrix 17.8 + 10.0 us with T3 in the same launch)
 constexpr int kSegmentedNlist = 8192;
+// nlist <= 1024: one fused coarse launch (keys in LDS); -DFUSED_COARSE=0 builds the
+// A/B variant with the key matrix + k_coarse_select
+#ifndef FUSED_COARSE
+#define FUSED_COARSE 1
+#endif
+constexpr bool kFusedCoarse = FUSED_COARSE;
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
@@ -774,6 +780,11 @@ struct ivfpq_index {
       if (T3out) launch_ip_table(x, c, d, d_cb.as<float>(), M, ksub, T3out, s);
       launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, W().w_cand.as<uint64_t>(),
                               dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
+      return plan != nullptr;
+    }
+    if (kFusedCoarse && coarse_fused_ok(nlist, d, np)) {  // keys in LDS, selection in the same launch
+      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, ip(), plan,
+                          d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>(), T3out, d_cb.as<float>(), M);
       return plan != nullptr;
     }
     W().w_dist.ensure(sizeof(float) * c * nlist);

@@ -47,6 +47,15 @@ void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, 
                           hipStream_t s, bool ip, const ListPlan* plan = nullptr, const int64_t* list_off = nullptr,
                           int lo = 0, int hi = 0, const float* x = nullptr, const float* cent = nullptr, int d = 0);
 
+// Fused coarse quantizer (nlist <= 1024, nprobe <= 64; coarse_fused_ok): per 16
+// queries the keys of every centroid in LDS and the selection + planning of
+// launch_coarse_select in the same launch, which also builds T3 when T3out is set.
+bool coarse_fused_ok(int nlist, int d, int nprobe);
+void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist, int nprobe,
+                         float* out_dis, int64_t* out_list, hipStream_t s, bool ip, const ListPlan* plan,
+                         const int64_t* list_off, int lo, int hi, const float* cent, float* T3out, const float* cb,
+                         int M);
+
 // Large-nlist coarse quantizer without the key matrix: per (16 queries,
 // centroid segment) the nprobe (<= 64) best (key, list) words on the matrix
 // cores (cand [nq][coarse_segments(nq, nlist)][nprobe]), then per query their

@@ -953,19 +953,13 @@ __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, i
 // once and merged into the running list.  With `cp.on`, the epilogue plans
 // the batch exactly as k_coarse_fused did (first usable probe, tau reset,
 // bucket entries with the scan's dis0).
-__global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__ keys, int64_t nq, int nlist,
-                                                       int nprobe, float* __restrict__ out_dis,
-                                                       int64_t* __restrict__ out_list, int ip,
-                                                       const float* __restrict__ x, int d, CoarsePlan cp) {
-  __shared__ uint64_t scratch[4][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
-  if (q >= nq) return;  // wave-uniform
-  const float* row = keys + q * nlist;
+// The nprobe (<= 64) smallest (key, list) words of one query's key row (global
+// or LDS), ascending across the wave (packed, kKcNone = none); scratch: 64 words
+// of LDS for this wave.
+__device__ __forceinline__ uint64_t coarse_select_row(const float* row, int nlist, int nprobe, uint64_t* scratch,
+                                                      int lane) {
   const uint64_t lt = (1ull << lane) - 1;
   uint64_t run = kKcNone;
-  SDIAG(0);
   for (int base = 0; base < nlist; base += 1024) {
     float v[16];
     float m = kInf;
@@ -975,25 +969,21 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
       v[u] = c < nlist ? row[c] : kInf;
       m = fminf(m, v[u]);
     }
-    SDIAG(1);
     const float T = wave_kth_smallest(m, nprobe, lane);
-    SDIAG(2);
     int total = 0;
-    bool fits = true;
 #pragma unroll
     for (int u = 0; u < 16; u++) {
       const int c = base + u * 64 + lane;
       const bool pass = c < nlist && v[u] <= T;
       const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
       const int pos = total + __popcll(mk & lt);
-      if (pass && pos < 64) scratch[wave][pos] = pack_kc(v[u], c);
+      if (pass && pos < 64) scratch[pos] = pack_kc(v[u], c);
       total += __popcll(mk);
     }
-    fits = total <= 64;
     uint64_t p;
-    if (fits) {
+    if (total <= 64) {
       __builtin_amdgcn_wave_barrier();
-      p = lane < total ? scratch[wave][lane] : kKcNone;
+      p = lane < total ? scratch[lane] : kKcNone;
       kc_sort64(p, lane);
       kc_merge64(run, p, lane);
     } else {  // many ties at the cut (rare): every 64-key slice of the block
@@ -1007,9 +997,113 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
     }
     __builtin_amdgcn_wave_barrier();  // scratch reuse
   }
+  return run;
+}
+
+__global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__ keys, int64_t nq, int nlist,
+                                                       int nprobe, float* __restrict__ out_dis,
+                                                       int64_t* __restrict__ out_list, int ip,
+                                                       const float* __restrict__ x, int d, CoarsePlan cp) {
+  __shared__ uint64_t scratch[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
+  if (q >= nq) return;  // wave-uniform
+  SDIAG(0);
+  const uint64_t run = coarse_select_row(keys + q * nlist, nlist, nprobe, scratch[wave], lane);
   SDIAG(3);
   coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
   SDIAG(5);
+}
+
+// Fused coarse quantizer for nlist <= kFusedCoarseLists (C2): workgroup = 16
+// queries x every centroid.  Its 4 waves compute the key tiles (the
+// coarse_key_tile MFMA arithmetic of k_coarse_gemm) for all nlist centroids
+// into LDS, then each wave selects and plans 4 of the queries from there
+// (coarse_select_row + coarse_emit, as k_coarse_select): the [B x nlist] key
+// matrix never goes through HBM and the selection needs no second launch.
+// Workgroups past the key blocks build T3 as in k_coarse_gemm.
+constexpr int kFusedCoarseLists = 1024;
+
+__global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
+                                                      const float* __restrict__ centT, int ldc,
+                                                      const float* __restrict__ cn, int nlist, int ip, int nprobe,
+                                                      float* __restrict__ out_dis, int64_t* __restrict__ out_list,
+                                                      int nkb, CoarseT3 t3, CoarsePlan cp) {
+  extern __shared__ __attribute__((aligned(16))) float g_lds[];
+  __shared__ uint64_t scratch[4][64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  if ((int)blockIdx.x >= nkb) {  // ---- T3 role (k_coarse_gemm's)
+    const int tb = blockIdx.x - nkb;
+    const int total = t3.M * 256;
+    const int dsub = d / t3.M;
+    const int64_t q0 = (int64_t)(tb / t3.M) * GQ;
+    const int m = tb % t3.M;
+    const int e = m * 256 + tid;
+    float* xs = g_lds;
+    for (int i = tid; i < GQ * dsub; i += 256) {
+      const int qq = i / dsub;
+      xs[i] = q0 + qq < nq ? x[(q0 + qq) * d + m * dsub + (i - qq * dsub)] : 0.f;
+    }
+    __syncthreads();
+    const int nqq = (int)min<int64_t>(GQ, nq - q0);
+    if (dsub == 8) {
+      const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
+      const float4 c0 = src[0], c1 = src[1];
+      const float w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int qq = 0; qq < GQ; qq++) {
+        const float4* xv = reinterpret_cast<const float4*>(xs + qq * 8);
+        const float4 x0 = xv[0], x1 = xv[1];
+        const float xq[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const float v = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
+        if (qq < nqq) t3.out[(q0 + qq) * total + e] = v;
+      }
+    } else {
+      const float* cwp = t3.cb + (int64_t)e * dsub;
+      for (int qq = 0; qq < nqq; qq++) {
+        const float* xq = xs + qq * dsub;
+        t3.out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
+      }
+    }
+    return;
+  }
+  // ---- keys of 16 queries x all centroids into LDS, then the selection
+  const int64_t q0 = (int64_t)blockIdx.x * GQ;
+  const int dk = (d + 63) & ~63;
+  float* xs = g_lds;            // [dk][GQ]
+  float* xn = xs + dk * GQ;     // [GQ] + 128 scratch
+  float* keys = xn + GQ * 9;    // [GQ][nlist]
+  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+  __syncthreads();  // xn
+  const int i16 = lane & 15, k4 = lane >> 4;
+  for (int cb = 0; cb < nlist; cb += GC) {
+    const int c0 = cb + wave * 32;
+    f4 acc[NTL];
+    coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
+#pragma unroll
+    for (int t = 0; t < NTL; t++) {
+      const int c = c0 + t * 16 + i16;
+      if (c >= nlist) continue;
+      const float cnv = ip ? 0.f : cn[c];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int i = k4 * 4 + r;
+        keys[i * nlist + c] = coarse_key(acc[t][r], xn[i], cnv, ip);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+    const int i = wave * 4 + r;
+    const int64_t q = q0 + i;
+    if (q >= nq) break;  // wave-uniform
+    const uint64_t run = coarse_select_row(keys + i * nlist, nlist, nprobe, scratch[wave], lane);
+    coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
+  }
 }
 
 // ------------------------------------------------------ linear pre-transform
@@ -3277,6 +3371,47 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
                      (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
 }
 
+bool coarse_fused_ok(int nlist, int d, int nprobe) {
+  const size_t smem = sizeof(float) * ((size_t)((d + 63) & ~63) * GQ + GQ * 9 + (size_t)GQ * nlist);
+  return nlist <= kFusedCoarseLists && nprobe <= 64 && smem <= 150 * 1024;
+}
+
+void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist, int nprobe,
+                         float* out_dis, int64_t* out_list, hipStream_t s, bool ip, const ListPlan* plan,
+                         const int64_t* list_off, int lo, int hi, const float* cent, float* T3out, const float* cb,
+                         int M) {
+  if (nq <= 0) return;
+  const unsigned nkb = nblocks(nq, GQ);
+  CoarseT3 t3;
+  if (T3out && M > 0 && d % M == 0) {
+    t3.out = T3out;
+    t3.cb = cb;
+    t3.M = M;
+    t3.nblk = (int)(nkb * (unsigned)M);
+  }
+  const size_t smem = sizeof(float) * ((size_t)((d + 63) & ~63) * GQ + GQ * 9 + (size_t)GQ * nlist);
+  {  // dynamic LDS above 64 KiB is opted into per device
+    static uint64_t attr_done = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 64 && !(attr_done & (1ull << dev))) {
+      (void)hipFuncSetAttribute((const void*)k_coarse_fused, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      attr_done |= 1ull << dev;
+    }
+  }
+  CoarsePlan cp;
+  if (plan) {
+    cp.pl = *plan;
+    cp.on = 1;
+    cp.list_off = list_off;
+    cp.lo = lo;
+    cp.hi = hi;
+    cp.cent = cent;
+  }
+  hipLaunchKernelGGL(k_coarse_fused, dim3(nkb + (unsigned)t3.nblk), dim3(256), smem, s, x, nq, d, centT,
+                     (nlist + 3) & ~3, cn, nlist, ip ? 1 : 0, nprobe, out_dis, out_list, (int)nkb, t3, cp);
+}
+
 int coarse_segments(int64_t nq, int nlist) {
   const int64_t qt = (nq + GQ - 1) / GQ;
   const int tiles = (nlist + GC - 1) / GC;
@@ -3435,9 +3570,10 @@ int scan_lists_grid(int M, int k) {
 }
 
 // the pipelined scan (k_scan_pipe) serves k <= 16 at M <= 16 with fused planning;
-// -DSCAN_PIPE=0 builds the A/B variant that runs k_scan_lists there instead
+// (off by default: one item per CU at a time measured slower than two
+// k_scan_lists workgroups per CU; -DSCAN_PIPE=1 builds it)
 #ifndef SCAN_PIPE
-#define SCAN_PIPE 1
+#define SCAN_PIPE 0
 #endif
 
 int device_cus() {
