@@ -1231,10 +1231,17 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
     const int p = p0 + lane;
     const int64_t l = p < nprobe ? lists[q * nprobe + p] : -1;
     bool use = p < nprobe && l >= lo && l < hi && list_off[l + 1] > list_off[l];
-    if (dedup && use) {
+    if (dedup) {
+      // an earlier probe with the same list: the earlier ones of this 64-probe
+      // block by readlane (lanes below this one), those of earlier blocks from memory
       bool dup = false;
-      for (int j = 0; j < p && !dup; j++) dup = lists[q * nprobe + j] == l;
-      if (dup) {  // the merge reads every usable pair's partial slots: write them empty
+      for (int j = 0; j < 64 && p0 + j < nprobe; j++) {
+        const int64_t lj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)l >> 32), j) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)l, j));
+        dup = dup || (j < lane && lj == l);
+      }
+      for (int j = 0; j < p0 && use && !dup; j++) dup = lists[q * nprobe + j] == l;
+      if (use && dup) {  // the merge reads every usable pair's partial slots: write them empty
         use = false;
         const int64_t o = (q * nprobe + p) * 4 * (int64_t)k;
         for (int e = 0; e < 4 * k; e++) {
