@@ -89,10 +89,10 @@ def parse():
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
-    p.add_argument("--inflight", type=int, default=1,
+    p.add_argument("--inflight", type=int, default=2,
                    help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 turns the "
                         "index's batches-in-flight mode on so that consecutive batches overlap, DESIGN.md "
-                        "section 4); 1 = one stream")
+                        "section 4); 1 = one batch at a time on one stream")
     return p.parse_args()
 
 
@@ -278,14 +278,20 @@ def main():
         avg_launch_ms = scan_avg_ms
         bytes_per_launch = bytes_per_step
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    isolated = None
-    if stages_serial and stages_serial["lists"][1] > 0:  # the same launches, one batch at a time
-        iso_ms = stages_serial["lists"][0] / stages_serial["lists"][1]
-        isolated = {"avg_launch_ms": iso_ms, "achieved": bytes_per_launch / (iso_ms * 1e-3) / 1e9,
-                    "frac": bytes_per_launch / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-                    "note": "same steps one batch at a time on one stream (ms_per_step_serial); in the timed region "
-                            f"{inflight} batches are in flight, so a launch shares the chip with the next batch's "
-                            "coarse step and scan start, and its event span is longer"}
+    overlapped = None
+    measured_on = "the timed region (one batch at a time)"
+    if stages_serial and stages_serial["lists"][1] > 0:
+        # Batches in flight: in the timed region a scan launch shares the chip with the
+        # next batch's coarse step and scan start, so its event span is not the kernel's
+        # own duration.  The roofline is taken from the same steps run one batch at a
+        # time right after the timed region (ms_per_step_serial); the overlapped span is
+        # reported beside it.
+        overlapped = {"avg_launch_ms": avg_launch_ms, "achieved": achieved, "frac": achieved / HBM_PEAK_GBPS,
+                      "note": f"scan-kernel event span in the timed region, {inflight} batches in flight"}
+        avg_launch_ms = stages_serial["lists"][0] / stages_serial["lists"][1]
+        achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        measured_on = ("the timed region's steps run again one batch at a time on one stream, right after it "
+                       "(HIP events around each scan launch)")
 
     # ---------------------------------------------------------- recall (rank 0)
     recall = None
@@ -408,9 +414,10 @@ def main():
                 "kernel": kernel,
                 "alg_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": avg_launch_ms,
+                "measured_on": measured_on,
                 "scan_stage": {"alg_bytes": bytes_per_step, "avg_ms": scan_avg_ms,
                                "achieved": bytes_per_step / (scan_avg_ms * 1e-3) / 1e9},
-                "isolated": isolated,
+                "overlapped": overlapped,
                 "end_to_end": {"alg_bytes": bytes_per_step, "ms_per_step": ms_per_step,
                                "achieved": bytes_per_step / (ms_per_step * 1e-3) / 1e9 if world == 1 else None},
             },
