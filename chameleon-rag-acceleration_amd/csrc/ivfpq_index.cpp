@@ -164,6 +164,11 @@ constexpr int kSegmentedNlist = 8192;
 #define FUSED_COARSE 1
 #endif
 constexpr bool kFusedCoarse = FUSED_COARSE;
+// large d (C3): 64-query x 128-centroid key tiles; -DTILED_COARSE=0 builds the A/B variant
+#ifndef TILED_COARSE
+#define TILED_COARSE 1
+#endif
+constexpr bool kTiledCoarse = TILED_COARSE;
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
@@ -222,6 +227,7 @@ struct ivfpq_index {
   // (DESIGN.md §4).
   struct Work {
     DevBuf w_dist, w_lists, w_dis0, w_T3, w_cand;  // w_cand: large-nlist coarse segment candidates
+    DevBuf w_qn;  // |x|^2 of the batch's queries (tiled coarse keys)
     DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
     uint32_t epoch = 0;  // tag of the last batch planned in this workspace (ListPlan::tauq)
     // every use records `done` on its stream; the slot's next user (on another
@@ -788,8 +794,9 @@ struct ivfpq_index {
       return plan != nullptr;
     }
     W().w_dist.ensure(sizeof(float) * c * nlist);
+    W().w_qn.ensure(sizeof(float) * c);
     launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, W().w_dist.as<float>(), s, ip(), T3out,
-                       d_cb.as<float>(), M);
+                       d_cb.as<float>(), M, kTiledCoarse ? W().w_qn.as<float>() : nullptr);
     if (np <= 64) {
       launch_coarse_select(W().w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
                            list_hi, x, d_cent.as<float>(), d);

@@ -872,6 +872,128 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   CDIAG(5);
 }
 
+// Coarse key matrix for large d (C3: d = 768, nlist = 4096): workgroup = 64
+// queries x 128 centroids, wave w = queries 16 w .. 16 w + 15 x all 128 centroids
+// (8 tiles of v_mfma_f32_16x16x4_f32).  A (64 x KC) and B (KC x 128) k-chunks are
+// staged in LDS, double-buffered, so each centroid column is read from L2 once per
+// 64 queries (k_coarse_gemm: once per 16) and each query row once per 128
+// centroids.  Every key still accumulates one ascending-k MFMA chain (the
+// oracle's fmaf order, as k_coarse_gemm); |x|^2 comes from k_row_norms (same
+// Faiss tree order as coarse_stage_queries).  Workgroups past the key tiles build
+// T3 as in k_coarse_gemm.
+constexpr int TQ = 64, TC = 128, TKC = 32;
+constexpr int TAS = TKC + 2;   // A row stride (floats): 2 mod 32 -> conflict-free MFMA A reads
+constexpr int TBS = TC + 16;   // B row stride: 16 mod 32 -> conflict-free B reads
+
+__device__ __forceinline__ void t3_role(const float* __restrict__ x, int64_t nq, int d, const CoarseT3& t3, int tb,
+                                        float* xs, int tid) {
+  const int total = t3.M * 256;
+  const int dsub = d / t3.M;
+  const int64_t q0 = (int64_t)(tb / t3.M) * GQ;
+  const int m = tb % t3.M;
+  const int e = m * 256 + tid;
+  for (int i = tid; i < GQ * dsub; i += 256) {
+    const int qq = i / dsub;
+    xs[i] = q0 + qq < nq ? x[(q0 + qq) * d + m * dsub + (i - qq * dsub)] : 0.f;
+  }
+  __syncthreads();
+  const int nqq = (int)min<int64_t>(GQ, nq - q0);
+  const float* cwp = t3.cb + (int64_t)e * dsub;
+  for (int qq = 0; qq < nqq; qq++) {
+    const float* xq = xs + qq * dsub;
+    t3.out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_coarse_gemm_tiled(const float* __restrict__ x, const float* __restrict__ xn,
+                                                           int64_t nq, int d, const float* __restrict__ centT,
+                                                           int ldc, const float* __restrict__ cn, int nlist,
+                                                           float* __restrict__ keys, int ip, int ngemm, CoarseT3 t3) {
+  __shared__ __attribute__((aligned(16))) float As[2][TQ * TAS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TKC * TBS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if ((int)blockIdx.x >= ngemm) {
+    t3_role(x, nq, d, t3, blockIdx.x - ngemm, &As[0][0], tid);
+    return;
+  }
+  const int nct = (nlist + TC - 1) / TC;
+  const int64_t q0 = (int64_t)(blockIdx.x / nct) * TQ;
+  const int c0 = (blockIdx.x % nct) * TC;
+  // staging: thread t loads A row (t >> 2), k offsets 8 (t & 3) .. + 7 and B row (t >> 3),
+  // columns 16 (t & 7) .. + 15; rows past nq / d and columns past nlist read as 0 / clamped
+  const int ar = tid >> 2, ak = (tid & 3) * 8;
+  const int br = tid >> 3, bc = (tid & 7) * 16;
+  const float* xrow = x + min<int64_t>(q0 + ar, nq - 1) * d;
+  const bool arow_ok = q0 + ar < nq;
+  // columns past the padded width: clamped per float4 (never written out)
+  const int bc0 = min(c0 + bc, ldc - 4), bc1 = min(c0 + bc + 4, ldc - 4), bc2 = min(c0 + bc + 8, ldc - 4),
+            bc3 = min(c0 + bc + 12, ldc - 4);
+  float4 ra0, ra1, rb0, rb1, rb2, rb3;
+#define TILE_LOAD(k0)                                                                                   \
+  {                                                                                                     \
+    const int kk_ = (k0) + ak;                                                                          \
+    const float4 z_ = make_float4(0.f, 0.f, 0.f, 0.f);                                                  \
+    ra0 = (arow_ok && kk_ < d) ? *reinterpret_cast<const float4*>(xrow + kk_) : z_;                     \
+    ra1 = (arow_ok && kk_ + 4 < d) ? *reinterpret_cast<const float4*>(xrow + kk_ + 4) : z_;             \
+    const float* bp_ = centT + (int64_t)min((k0) + br, d - 1) * ldc;                                    \
+    rb0 = *reinterpret_cast<const float4*>(bp_ + bc0);                                                  \
+    rb1 = *reinterpret_cast<const float4*>(bp_ + bc1);                                                  \
+    rb2 = *reinterpret_cast<const float4*>(bp_ + bc2);                                                  \
+    rb3 = *reinterpret_cast<const float4*>(bp_ + bc3);                                                  \
+  }
+#define TILE_STORE(b)                                                                                   \
+  {                                                                                                     \
+    float2* ap_ = reinterpret_cast<float2*>(&As[b][ar * TAS + ak]);                                     \
+    ap_[0] = make_float2(ra0.x, ra0.y);                                                                 \
+    ap_[1] = make_float2(ra0.z, ra0.w);                                                                 \
+    ap_[2] = make_float2(ra1.x, ra1.y);                                                                 \
+    ap_[3] = make_float2(ra1.z, ra1.w);                                                                 \
+    float4* bq_ = reinterpret_cast<float4*>(&Bs[b][br * TBS + bc]);                                     \
+    bq_[0] = rb0;                                                                                       \
+    bq_[1] = rb1;                                                                                       \
+    bq_[2] = rb2;                                                                                       \
+    bq_[3] = rb3;                                                                                       \
+  }
+  f4 acc[TC / 16];
+#pragma unroll
+  for (int t = 0; t < TC / 16; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+  const int i16 = lane & 15, k4 = lane >> 4;
+  const int nk = (d + TKC - 1) / TKC;
+  TILE_LOAD(0);
+  TILE_STORE(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; kc++) {
+    const int b = kc & 1;
+    if (kc + 1 < nk) TILE_LOAD((kc + 1) * TKC);  // in flight during this chunk's MFMAs
+    const float* A = &As[b][(wave * 16 + i16) * TAS];
+    const float* B = &Bs[b][0];
+#pragma unroll
+    for (int j = 0; j < TKC / 4; j++) {
+      const int kk = 4 * j + k4;
+      const float av = A[kk];
+#pragma unroll
+      for (int t = 0; t < TC / 16; t++)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, B[kk * TBS + t * 16 + i16], acc[t], 0, 0, 0);
+    }
+    if (kc + 1 < nk) TILE_STORE(b ^ 1);
+    __syncthreads();
+  }
+#undef TILE_LOAD
+#undef TILE_STORE
+#pragma unroll
+  for (int t = 0; t < TC / 16; t++) {
+    const int c = c0 + t * 16 + i16;
+    if (c >= nlist) continue;
+    const float cnv = ip ? 0.f : cn[c];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int64_t q = q0 + wave * 16 + k4 * 4 + r;
+      if (q >= nq) continue;
+      keys[q * nlist + c] = coarse_key(acc[t][r], ip ? 0.f : xn[q], cnv, ip);
+    }
+  }
+}
+
 // T3 on the matrix cores -- a tolerance-mode A/B build only (-DT3_MFMA via
 // profiles/build_variants.sh; never the shipped library).  T3[q][m][j] =
 // <x_q[m], C_mj> as one 16 x 16 v_mfma_f32_16x16x4_f32 tile per (16 queries,
@@ -3346,9 +3468,27 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
   }
 }
 
+bool coarse_tiled_ok(int d, int64_t nq) { return d % 4 == 0 && d >= 256 && nq >= 64; }
+
 void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                        float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M) {
+                        float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M, float* xn_buf) {
   if (nq <= 0) return;
+  if (xn_buf && coarse_tiled_ok(d, nq)) {  // large d: 64-query x 128-centroid tiles, k-chunks staged in LDS
+    if (!ip) hipLaunchKernelGGL(k_row_norms, dim3(nblocks(nq, 256)), dim3(256), 0, s, x, nq, d, xn_buf);
+    const int ngemm = (int)(nblocks(nq, TQ) * nblocks(nlist, TC));
+    CoarseT3 t3;
+    if (T3out && M > 0 && d % M == 0 && d / M <= 2 * TQ * TAS / GQ) {
+      t3.out = T3out;
+      t3.cb = cb;
+      t3.M = M;
+      t3.nblk = (int)(nblocks(nq, GQ) * (unsigned)M);
+    } else if (T3out) {
+      launch_ip_table(x, nq, d, cb, M, 256, T3out, s);
+    }
+    hipLaunchKernelGGL(k_coarse_gemm_tiled, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), 0, s, x, xn_buf, nq, d,
+                       centT, (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
+    return;
+  }
   const unsigned nqb = nblocks(nq, GQ);
   const int ngemm = (int)(nqb * nblocks(nlist, GC));
   CoarseT3 t3;

@@ -270,6 +270,29 @@ def test_segmented_coarse_matches_oracle(nq, nprobe):
     np.testing.assert_array_equal(Dq.cpu().numpy(), Dr)
 
 
+@pytest.mark.parametrize("d,nlist,nq,metric", [(768, 4096, 200, 1), (260, 1102, 64, 1), (768, 1500, 129, 0),
+                                               (256, 2048, 1000, 0)])
+def test_tiled_coarse_matches_oracle(d, nlist, nq, metric):
+    """d >= 256 with 1024 < nlist < 8192 takes the 64-query x 128-centroid tiled
+    key GEMM (C3's coarse step); d = 260 leaves a partial k-chunk, nlist = 1102 a
+    partial centroid tile and a padded transposed row, nq = 129 / 200 a partial
+    query tile.  Gaussian data, so the keys' rounding order is what is tested."""
+    import torch
+
+    rng = np.random.default_rng(11)
+    M = 4
+    cent = rng.standard_normal((nlist, d), dtype=np.float32)
+    cent[77] = cent[901]  # an exact tie: ordered by list id
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, metric, device=0)
+    ix.set_trained(cent, rng.standard_normal((M, 256, d // M), dtype=np.float32))
+    ix.nprobe = 32
+    xq = rng.standard_normal((nq, d), dtype=np.float32)
+    Dq, Iq = ix.coarse_device(torch.from_numpy(xq).cuda())
+    Dr, Ir = O.coarse_search(xq, cent, 32, metric=metric)
+    np.testing.assert_array_equal(Iq.cpu().numpy(), Ir)
+    np.testing.assert_array_equal(Dq.cpu().numpy(), Dr)
+
+
 @pytest.mark.parametrize("k", [10, 100])
 def test_c4_shape_eight_list_range_shards(c4_shape, k):
     """C4's list-sharded form at its shape (d 96, M 48, nlist 65536, nprobe 32)
