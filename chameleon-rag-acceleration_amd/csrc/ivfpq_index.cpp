@@ -158,10 +158,11 @@ constexpr size_t kPartialBytes = size_t(2048) << 20;  // bound for a chunk's per
 // C2, nlist 1024: segmented 22.5 + 8.5 us + a separate T3 launch 13.0 us vs key
 // matrix 17.8 + 10.0 us with T3 in the same launch)
 constexpr int kSegmentedNlist = 8192;
-// nlist <= 1024: one fused coarse launch (keys in LDS); -DFUSED_COARSE=0 builds the
-// A/B variant with the key matrix + k_coarse_select
+// nlist <= 1024: one fused coarse launch (keys in LDS) with -DFUSED_COARSE=1 -- an A/B
+// variant only: at C2 it takes 54 us per batch against 30 us for the key matrix +
+// k_coarse_select (64 workgroups of 16 queries cannot fill the chip; profiles/r04_ab.txt)
 #ifndef FUSED_COARSE
-#define FUSED_COARSE 1
+#define FUSED_COARSE 0
 #endif
 constexpr bool kFusedCoarse = FUSED_COARSE;
 // large d (C3): 64-query x 128-centroid key tiles; -DTILED_COARSE=0 builds the A/B variant

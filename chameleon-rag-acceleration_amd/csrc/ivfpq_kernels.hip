@@ -467,12 +467,49 @@ __device__ __forceinline__ int f2ord(float f) {
 __device__ __forceinline__ float ord2f(int o) { return __int_as_float(o >= 0 ? o : o ^ 0x7FFFFFFF); }
 
 // ------------------------------------------------------------------ norms
-__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ x, int64_t n, int d,
-                                                   float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const float* xi = x + i * d;
-  out[i] = tree<K_NORM>([&](int t) { return xi[t]; }, [&](int t) { return xi[t]; }, d);
+// Eight lanes per row (8 rows per 64-thread workgroup): lane j of a row's group
+// holds tree()'s accumulator a8[j] (elements j, j + 8, ... in order), so a 768-d
+// row is 96 dependent adds per lane instead of 768 in one thread; the group's
+// combine, the 4-wide remainder and the masked tail then follow tree() exactly.
+__global__ __launch_bounds__(64) void k_row_norms(const float* __restrict__ x, int64_t n, int d,
+                                                  float* __restrict__ out) {
+  const int lane = threadIdx.x, j = lane & 7;
+  const int64_t i = (int64_t)blockIdx.x * 8 + (lane >> 3);
+  const bool ok = i < n;
+  const float* xi = x + (ok ? i : 0) * d;
+  const int d8 = d & ~7;
+  float a = 0.f;
+  int t = 0;
+  if (ok) {
+    for (; t + 32 <= d8; t += 32) {  // four loads in flight per lane, adds in element order
+      const float v0 = xi[t + j], v1 = xi[t + 8 + j], v2 = xi[t + 16 + j], v3 = xi[t + 24 + j];
+      a = a + v0 * v0;
+      a = a + v1 * v1;
+      a = a + v2 * v2;
+      a = a + v3 * v3;
+    }
+    for (; t < d8; t += 8) {
+      const float v = xi[t + j];
+      a = a + v * v;
+    }
+  }
+  const float hi4 = __shfl_down(a, 4, 8);  // a8[j + 4] for j < 4
+  float a4 = hi4 + a;                       // a4[j] = a8[j + 4] + a8[j]
+  int r = d8;
+  if (r + 4 <= d) {  // the 4-wide remainder
+    if (ok && j < 4) {
+      const float v = xi[r + j];
+      a4 = a4 + v * v;
+    }
+    r += 4;
+  }
+  if (ok && j < 4 && r + j < d) {  // the masked tail
+    const float v = xi[r + j];
+    a4 = a4 + v * v;
+  }
+  const float h = a4 + __shfl_down(a4, 1, 8);  // lane 0: a4[0] + a4[1], lane 2: a4[2] + a4[3]
+  const float h1 = __shfl_down(h, 2, 8);
+  if (ok && j == 0) out[i] = h + h1;
 }
 
 // ------------------------------------------------- coarse key matrix (split path)
@@ -3444,7 +3481,7 @@ inline int rows_for(int k) { return k <= 64 ? 1 : k <= 128 ? 2 : k <= 256 ? 4 : 
 
 void launch_row_norms(const float* x, int64_t n, int d, float* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_row_norms, dim3(nblocks(n, 256)), dim3(256), 0, s, x, n, d, out);
+  hipLaunchKernelGGL(k_row_norms, dim3(nblocks(n, 8)), dim3(64), 0, s, x, n, d, out);
 }
 
 void launch_l2_dist(const float* x, const float* xn, int64_t nx, const float* c, const float* cn, int nc, int d,
@@ -3474,7 +3511,7 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
                         float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M, float* xn_buf) {
   if (nq <= 0) return;
   if (xn_buf && coarse_tiled_ok(d, nq)) {  // large d: 64-query x 128-centroid tiles, k-chunks staged in LDS
-    if (!ip) hipLaunchKernelGGL(k_row_norms, dim3(nblocks(nq, 256)), dim3(256), 0, s, x, nq, d, xn_buf);
+    if (!ip) launch_row_norms(x, nq, d, xn_buf, s);
     const int ngemm = (int)(nblocks(nq, TQ) * nblocks(nlist, TC));
     CoarseT3 t3;
     if (T3out && M > 0 && d % M == 0 && d / M <= 2 * TQ * TAS / GQ) {
