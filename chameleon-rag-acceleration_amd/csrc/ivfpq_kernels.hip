@@ -3432,6 +3432,173 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   if (lane == 0) pl.qdone[q] = 1;
 }
 
+// ------------------------------------------- probe merge, k > 64, small L k
+// One 256-thread workgroup per query when its L = 4 nprobe partial lists hold
+// at most kRadixU x 256 entries (C2 at k = 100: 6400).  Every key is loaded with
+// one coalesced pass (the lists are contiguous: entry (j, i) at (qb + j) k + i)
+// into registers; the exact k-th smallest key T comes from a 4-pass MSB-first
+// radix select (8-bit digits, LDS histogram, equal digits of a wave counted by
+// one ballot); the entries <= T (the k best and every tie at T) are compacted,
+// labelled and sorted by (key, label).  No dependent global round trips beyond
+// the key load, the positions and the labels (k_merge_big: about a dozen).
+// Queries whose ties overflow kRadixCap are left to k_merge_probes' full merge.
+constexpr int kRadixU = 32;
+constexpr int kRadixCap = 512;
+
+__global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
+  __shared__ int s_len[256];
+  __shared__ int s_hist[256];
+  __shared__ int s_wsum[4];
+  __shared__ int s_sel[2];
+  __shared__ int s_n;
+  __shared__ float cd[kRadixCap];
+  __shared__ int64_t cl[kRadixCap];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t q = blockIdx.x;
+  const int k = a.k, np = a.nprobe, L = 4 * np;
+  const uint64_t qm = pl.qmask[q];
+  const int64_t qb = q * (int64_t)L;
+  const float pad = a.ip ? -FLT_MAX : FLT_MAX;
+  const float sgn = a.ip ? -1.f : 1.f;
+  const uint64_t lt = (1ull << lane) - 1;
+  {
+    int n = 0;
+    if (tid < L && ((qm >> (tid >> 2)) & 1)) {
+      n = pl.partN[qb + tid];
+      if (n < 0 || n > k) {  // a partial list holds at most k entries
+        atomicAdd(pl.err, 1);
+        n = 0;
+      }
+    }
+    s_len[tid] = n;
+    const int ws = wave_sum_i(n);
+    if (lane == 0) s_wsum[wave] = ws;
+  }
+  __syncthreads();
+  const int C = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  const int E = L * k;
+  const float inv_k = 1.0f / (float)k;
+  const float* pd = pl.partD + qb * k;
+  uint32_t key[kRadixU];
+#pragma unroll
+  for (int u = 0; u < kRadixU; u++) {
+    const int e = u * 256 + tid;
+    key[u] = 0xFFFFFFFFu;  // absent (no finite key maps here)
+    if (e < E) {
+      const int j = div_small(e, k, inv_k);
+      if (e - j * k < s_len[j]) key[u] = ukey_of(pd[e]);
+    }
+  }
+  // the k-th smallest present key (all of them when there are at most k)
+  uint32_t T = 0xFFFFFFFEu;
+  if (C > k) {
+    uint32_t prefix = 0;
+    int r = k;  // rank of the k-th key among the keys matching the prefix
+#pragma unroll 1
+    for (int pass = 0; pass < 4; pass++) {
+      const int shift = 24 - 8 * pass;
+      s_hist[tid] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kRadixU; u++) {
+        if (u * 256 >= E) break;  // block-uniform
+        const uint32_t kv = key[u];
+        const bool m = kv != 0xFFFFFFFFu && (pass == 0 || (kv >> (shift + 8)) == (prefix >> (shift + 8)));
+        const int bin = (int)((kv >> shift) & 255u);
+        uint64_t act = __builtin_amdgcn_ballot_w64(m);
+        // lanes sharing the first active lane's digit: one LDS add for all of them
+        // (keys of one query mostly share their high digits); the rest add singly
+        if (act) {
+          const int l0 = (int)__builtin_ctzll(act);
+          const int b0 = __builtin_amdgcn_readlane(bin, l0);
+          const uint64_t same = __builtin_amdgcn_ballot_w64(m && bin == b0);
+          if (lane == l0) atomicAdd(&s_hist[b0], (int)__popcll(same));
+          if (m && bin != b0) atomicAdd(&s_hist[bin], 1);
+        }
+      }
+      __syncthreads();
+      const int h = s_hist[tid];
+      const int iw = wave_incl_scan(h, lane);
+      if (lane == 63) s_wsum[wave] = iw;
+      __syncthreads();
+      int incl = iw;
+      for (int w = 0; w < wave; w++) incl += s_wsum[w];
+      if (incl >= r && incl - h < r) {
+        s_sel[0] = tid;
+        s_sel[1] = r - (incl - h);
+      }
+      __syncthreads();
+      prefix |= (uint32_t)s_sel[0] << shift;
+      r = s_sel[1];
+      __syncthreads();  // s_wsum / s_sel are rewritten by the next pass
+    }
+    T = prefix;
+  }
+  // compact the entries <= T (positions from partI)
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+  const int64_t* pi = pl.partI + qb * k;
+#pragma unroll
+  for (int u = 0; u < kRadixU; u++) {
+    if (u * 256 >= E) break;  // block-uniform
+    const bool c = key[u] <= T;
+    const uint64_t mk = __builtin_amdgcn_ballot_w64(c);
+    if (!mk) continue;  // wave-uniform
+    int base = 0;
+    if (lane == (int)__builtin_ctzll(mk)) base = atomicAdd(&s_n, (int)__popcll(mk));
+    base = __builtin_amdgcn_readlane(base, (int)__builtin_ctzll(mk));
+    const int at = base + (int)__popcll(mk & lt);
+    if (c && at < kRadixCap) {
+      const int e = u * 256 + tid;
+      cd[at] = pd[e];
+      cl[at] = pi[e];
+    }
+  }
+  __syncthreads();
+  const int n = s_n;
+  if (n > kRadixCap) return;  // ties overflow: the full merge of k_merge_probes takes this query
+  int P = 64;
+  while (P < n) P <<= 1;
+  for (int e = tid; e < P; e += 256) {
+    if (e < n) {
+      const int64_t pos = cl[e];
+      cl[e] = pos_ok(a, pl, pos) ? a.ids[pos] : kSentinelId;
+    } else {
+      cd[e] = kInf;
+      cl[e] = kSentinelId;
+    }
+  }
+  __syncthreads();
+  // bitonic sort of P entries by (key, label), ascending
+  for (int sz = 2; sz <= P; sz <<= 1) {
+    for (int st = sz >> 1; st > 0; st >>= 1) {
+      for (int p0 = 0; p0 < P / 2; p0 += 256) {
+        const int pi2 = p0 + tid;
+        if (pi2 < P / 2) {
+          const int i = ((pi2 / st) * 2 * st) + (pi2 % st);
+          const int j = i + st;
+          const bool up = (i & sz) == 0;
+          const float di = cd[i], dj = cd[j];
+          const int64_t li = cl[i], lj = cl[j];
+          if (lexless(dj, lj, di, li) == up) {
+            cd[i] = dj;
+            cl[i] = lj;
+            cd[j] = di;
+            cl[j] = li;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int e = tid; e < k; e += 256) {
+    const bool empty = e >= n;
+    a.outD[q * k + e] = empty ? pad : sgn * cd[e];
+    a.outI[q * k + e] = empty ? -1 : cl[e];
+  }
+  if (tid == 0) pl.qdone[q] = 1;
+}
+
 // ------------------------------------------------------------ shard merge
 __global__ __launch_bounds__(256) void k_merge_topk(int S, int64_t n, int k, const float* __restrict__ Din,
                                                     const int64_t* __restrict__ Iin, float* __restrict__ Dout,
@@ -3795,7 +3962,12 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
     hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   }
   if (ev) (void)hipEventRecord(ev[1], s);
-  if (R >= 2 && a.nprobe <= 64) hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
+  if (R >= 2 && a.nprobe <= 64) {
+    if (4 * a.nprobe * a.k <= kRadixU * 256)  // every key of a query in one workgroup's registers
+      hipLaunchKernelGGL(k_merge_radix, dim3((unsigned)a.nq), dim3(256), 0, s, a, pl);
+    else
+      hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
+  }
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
 }
 
