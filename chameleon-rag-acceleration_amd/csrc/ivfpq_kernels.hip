@@ -3501,9 +3501,8 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
       __syncthreads();
 #pragma unroll
       for (int u = 0; u < kRadixU; u++) {
-        if (u * 256 >= E) break;  // block-uniform
         const uint32_t kv = key[u];
-        const bool m = kv != 0xFFFFFFFFu && (pass == 0 || (kv >> (shift + 8)) == (prefix >> (shift + 8)));
+        const bool m = u * 256 < E && kv != 0xFFFFFFFFu && (pass == 0 || (kv >> (shift + 8)) == (prefix >> (shift + 8)));
         const int bin = (int)((kv >> shift) & 255u);
         uint64_t act = __builtin_amdgcn_ballot_w64(m);
         // lanes sharing the first active lane's digit: one LDS add for all of them
@@ -3540,8 +3539,7 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
   const int64_t* pi = pl.partI + qb * k;
 #pragma unroll
   for (int u = 0; u < kRadixU; u++) {
-    if (u * 256 >= E) break;  // block-uniform
-    const bool c = key[u] <= T;
+    const bool c = key[u] <= T;  // (absent keys: 0xFFFFFFFF > T)
     const uint64_t mk = __builtin_amdgcn_ballot_w64(c);
     if (!mk) continue;  // wave-uniform
     int base = 0;

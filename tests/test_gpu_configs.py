@@ -270,17 +270,17 @@ def test_segmented_coarse_matches_oracle(nq, nprobe):
     np.testing.assert_array_equal(Dq.cpu().numpy(), Dr)
 
 
-@pytest.mark.parametrize("d,nlist,nq,metric", [(768, 4096, 200, 1), (260, 1102, 64, 1), (768, 1500, 129, 0),
+@pytest.mark.parametrize("d,nlist,nq,metric", [(768, 4096, 200, 1), (264, 1102, 64, 1), (768, 1500, 129, 0),
                                                (256, 2048, 1000, 0)])
 def test_tiled_coarse_matches_oracle(d, nlist, nq, metric):
     """d >= 256 with 1024 < nlist < 8192 takes the 64-query x 128-centroid tiled
-    key GEMM (C3's coarse step); d = 260 leaves a partial k-chunk, nlist = 1102 a
+    key GEMM (C3's coarse step); d = 264 leaves a partial k-chunk, nlist = 1102 a
     partial centroid tile and a padded transposed row, nq = 129 / 200 a partial
     query tile.  Gaussian data, so the keys' rounding order is what is tested."""
     import torch
 
     rng = np.random.default_rng(11)
-    M = 4
+    M = 8
     cent = rng.standard_normal((nlist, d), dtype=np.float32)
     cent[77] = cent[901]  # an exact tie: ordered by list id
     ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, metric, device=0)
