@@ -2482,6 +2482,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     it_no++;
     cur = nxt;
   }
+#ifdef SCAN_REL
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // A/B: coherence experiment
+#endif
 }
 
 // ------------------------------------------ pipelined list scan (k <= 16)
@@ -3444,8 +3447,14 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
 // Queries whose ties overflow kRadixCap are left to k_merge_probes' full merge.
 constexpr int kRadixU = 32;
 constexpr int kRadixCap = 512;
+#ifndef MERGE_RADIX
+#define MERGE_RADIX 1  // -DMERGE_RADIX=0: k_merge_big for every k > 64 (A/B variant)
+#endif
 
 __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
+#ifdef MERGE_ACQ
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // A/B: coherence experiment
+#endif
   __shared__ int s_len[256];
   __shared__ int s_hist[256];
   __shared__ int s_wsum[4];
@@ -3961,7 +3970,7 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   }
   if (ev) (void)hipEventRecord(ev[1], s);
   if (R >= 2 && a.nprobe <= 64) {
-    if (4 * a.nprobe * a.k <= kRadixU * 256)  // every key of a query in one workgroup's registers
+    if (MERGE_RADIX && 4 * a.nprobe * a.k <= kRadixU * 256)  // every key of a query in one workgroup's registers
       hipLaunchKernelGGL(k_merge_radix, dim3((unsigned)a.nq), dim3(256), 0, s, a, pl);
     else
       hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);

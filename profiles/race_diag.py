@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Batches-in-flight mismatch hunt (tests/test_gpu_parity.py
+test_batches_in_flight_on_round_robin_streams scenario): the rr_index index
+(IVF256,PQ8, d 64, nprobe 12), 24 batches of 256 queries issued round robin on
+several streams with the handle's inflight mode on, compared with each batch
+searched alone.  Per (k, streams, round): mismatching batches / rows, whether
+the bad rows hold sentinel labels or non-finite keys, and the merge kernels'
+index-check count.  Round 0 of each configuration is the first use of the
+workspaces at that k (buffers grow there); later rounds reuse them.
+Prints one JSON line per configuration."""
+import json
+import os
+import sys
+import time
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(R, "chameleon-rag-acceleration_amd"))
+
+
+def main():
+    import numpy as np
+    import torch
+
+    import faiss_amd as faiss
+    from faiss_amd import datasets
+
+    configs = [(100, 3), (100, 2), (10, 3), (100, 4)]
+    if len(sys.argv) > 1:
+        configs = [tuple(int(v) for v in c.split(",")) for c in sys.argv[1:]]
+    rounds = int(os.environ.get("RACE_ROUNDS", "8"))
+    xt = datasets.synthetic_sift_like(20_000, 64, seed=4321, n_centres=20_000)
+    xb = datasets.synthetic_sift_like(100_000, 64, seed=1234, n_centres=20_000)
+    xq = datasets.synthetic_sift_like(24 * 256, 64, seed=123, n_centres=20_000)
+    ix = faiss.index_factory(64, "IVF256,PQ8", device=0)
+    ix.niter_coarse = ix.niter_pq = 8
+    ix.train(xt)
+    ix.add(xb)
+    ix.nprobe = 12
+    nb = 24
+    xd = torch.from_numpy(xq).cuda().view(nb, 256, 64)
+    torch.cuda.synchronize()
+    refs = {}
+    for k in sorted({c[0] for c in configs}):
+        ref = []
+        for b in range(nb):
+            D, I = ix.search_device(xd[b], k)
+            torch.cuda.synchronize()
+            ref.append((D.cpu().numpy(), I.cpu().numpy()))
+        refs[k] = ref
+    big = np.iinfo(np.int64).max
+    for k, nst in configs:
+        t0 = time.time()
+        streams = [torch.cuda.Stream() for _ in range(nst)]
+        per_round = []
+        detail = None
+        for rnd in range(rounds):
+            e0 = ix.error_count()
+            outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
+                    for _ in range(nb)]
+            ix.inflight = True
+            try:
+                torch.cuda.synchronize()
+                for b in range(nb):
+                    ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=streams[b % nst].cuda_stream)
+                torch.cuda.synchronize()
+            finally:
+                ix.inflight = False
+            bad_b, bad_rows, sent, nonfin = 0, 0, 0, 0
+            for b in range(nb):
+                D = outs[b][0].cpu().numpy()
+                I = outs[b][1].cpu().numpy()
+                Dr, Ir = refs[k][b]
+                rows = np.nonzero((I != Ir).any(axis=1) | (D != Dr).any(axis=1))[0]
+                if len(rows):
+                    bad_b += 1
+                    bad_rows += len(rows)
+                    sent += int((I[rows] == big).sum())
+                    nonfin += int((~np.isfinite(D[rows])).sum())
+                    if detail is None:
+                        r = int(rows[0])
+                        diff = np.nonzero((I[r] != Ir[r]) | (D[r] != Dr[r]))[0]
+                        detail = {"round": rnd, "batch": b, "stream": b % nst, "row": r, "rows": rows[:8].tolist(),
+                                  "first_diff_rank": int(diff[0]), "n_diff": int(len(diff)),
+                                  "I": I[r, diff[:6]].tolist(), "I_ref": Ir[r, diff[:6]].tolist(),
+                                  "D": D[r, diff[:6]].tolist(), "D_ref": Dr[r, diff[:6]].tolist()}
+            per_round.append({"bad_batches": bad_b, "bad_rows": bad_rows, "sentinels": sent, "nonfinite": nonfin,
+                              "err": ix.error_count() - e0})
+        print(json.dumps({"k": k, "streams": nst, "rounds": rounds, "per_round": per_round, "first": detail,
+                          "s": round(time.time() - t0, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
