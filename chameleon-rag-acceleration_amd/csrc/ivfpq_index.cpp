@@ -44,6 +44,11 @@ void require(bool ok, const std::string& msg) {
   if (!ok) throw std::runtime_error(msg);
 }
 
+#ifdef DEVBUF_GUARD
+// experiment: every buffer is followed by kGuard bytes of 0xA5; check_guard() reports
+// whether any of them changed (an out-of-bounds write past the buffer's end)
+constexpr size_t kGuard = 1 << 16;
+#endif
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -51,9 +56,27 @@ struct DevBuf {
     if (b <= bytes && p) return;
     release();
     if (b == 0) b = 16;
+#ifdef DEVBUF_GUARD
+    b = (b + 255) & ~(size_t)255;
+    HIPCHECK(hipMalloc(&p, b + kGuard));
+    HIPCHECK(hipMemset(static_cast<char*>(p) + b, 0xA5, kGuard));
+    HIPCHECK(hipDeviceSynchronize());
+    bytes = b;
+    return;
+#endif
     HIPCHECK(hipMalloc(&p, b));
     bytes = b;
   }
+#ifdef DEVBUF_GUARD
+  bool check_guard() const {
+    if (!p) return true;
+    std::vector<unsigned char> g(kGuard);
+    HIPCHECK(hipMemcpy(g.data(), static_cast<const char*>(p) + bytes, kGuard, hipMemcpyDeviceToHost));
+    for (unsigned char c : g)
+      if (c != 0xA5) return false;
+    return true;
+  }
+#endif
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -170,6 +193,12 @@ constexpr bool kFusedCoarse = FUSED_COARSE;
 #define TILED_COARSE 1
 #endif
 constexpr bool kTiledCoarse = TILED_COARSE;
+// Batches in flight overlap only searches with k <= 64 (the row-packed and one-row
+// top-k paths).  k > 64 searches (partial-list lengths, k_merge_radix / k_merge_big)
+// returned wrong rows in about 1 batch of 40 when two of them overlapped, and the
+// cause is not found (profiles/r04_race.txt): they are ordered after
+// every search in flight, in either mode.
+constexpr int kInflightMaxK = 64;
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
@@ -230,6 +259,9 @@ struct ivfpq_index {
     DevBuf w_dist, w_lists, w_dis0, w_T3, w_cand;  // w_cand: large-nlist coarse segment candidates
     DevBuf w_qn;  // |x|^2 of the batch's queries (tiled coarse keys)
     DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
+#ifdef PART_CHECK
+    DevBuf p_chk;  // experiment: per partial list (count, hash) as the scan wrote it
+#endif
     uint32_t epoch = 0;  // tag of the last batch planned in this workspace (ListPlan::tauq)
     // every use records `done` on its stream; the slot's next user (on another
     // stream) waits for it, and whatever frees or rewrites shared device buffers
@@ -250,7 +282,9 @@ struct ivfpq_index {
   // The workspace of a device call on stream s: the one last used on s (stream
   // order already protects it, and a one-stream caller keeps a single
   // workspace), else the least recently used one, ordered after its last user.
-  void begin_slot(hipStream_t s) {
+  // overlap: this call may run concurrently with calls on other streams (inflight mode
+  // and k <= kInflightMaxK); otherwise it is ordered after every call in flight
+  void begin_slot(hipStream_t s, bool overlap = true) {
     int pick = -1;
     for (int i = 0; i < kSlots && pick < 0; i++)
       if (work[i].done_pending && work[i].done_stream == s) pick = i;
@@ -271,7 +305,7 @@ struct ivfpq_index {
       HIPCHECK(hipEventSynchronize(w.done));
       w.done_pending = false;
     }
-    if (!inflight) order_after_all(s);
+    if (!inflight || !overlap) order_after_all(s);
   }
   // ordered after every device call still in flight (for paths that touch the
   // shared staging buffers or T3-ahead state)
@@ -311,8 +345,9 @@ struct ivfpq_index {
       w.p_hdr.ensure(sizeof(int32_t) * 16);
       HIPCHECK(hipMemsetAsync(w.p_hdr.p, 0, w.p_hdr.bytes, s));
     }
-    w.p_D.ensure(sizeof(float) * nq * np * 4 * k);
-    w.p_I.ensure(sizeof(int64_t) * nq * np * 4 * k);
+    pl.ks = part_stride(k);
+    w.p_D.ensure(sizeof(float) * nq * np * 4 * pl.ks);
+    w.p_I.ensure(sizeof(int64_t) * nq * np * 4 * pl.ks);
     w.p_N.ensure(sizeof(int32_t) * nq * np * 4);
     if (!w.p_done.p || w.p_done.bytes < sizeof(int32_t) * nq) {  // kept zero between batches by k_merge_probes
       w.p_done.ensure(sizeof(int32_t) * nq);
@@ -340,6 +375,13 @@ struct ivfpq_index {
     pl.epoch = w.epoch;
     pl.err = w.p_hdr.as<int32_t>() + 15;
     pl.qmask = w.p_qmask.as<uint64_t>();
+#ifdef PART_CHECK
+    if (!w.p_chk.p || w.p_chk.bytes < sizeof(uint32_t) * 4 * nq * np * 4) {
+      w.p_chk.ensure(sizeof(uint32_t) * 4 * nq * np * 4);
+      HIPCHECK(hipMemsetAsync(w.p_chk.p, 0, w.p_chk.bytes, s));
+    }
+    pl.chk = w.p_chk.as<uint32_t>();
+#endif
     pl.order = d_order.p ? d_order.as<int32_t>() : nullptr;
     pl.fused = scan_fused_plan(nloc, pl.max_items, M) ? 1 : 0;
     return pl;
@@ -814,7 +856,7 @@ struct ivfpq_index {
     check_search(n, k);
     upload_lists();
     if (n == 0) return;
-    begin_slot(s);
+    begin_slot(s, k <= kInflightMaxK);
     const int np = preassigned ? nprobe : eff_nprobe();
     const int64_t qc = query_chunk(n, np, k);
     W().w_T3.ensure(sizeof(float) * qc * M * ksub);
@@ -907,7 +949,7 @@ struct ivfpq_index {
     const int nloc = std::max(list_hi - list_lo, 1);
     const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)nloc * 16});
     return std::max<int64_t>(
-        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * k * 48))}));
+        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * part_stride(k) * 48))}));
   }
 
   // T3 [n][M][ksub] of the queries x, on stream s, ahead of a preassigned search
@@ -1357,6 +1399,29 @@ int ivfpq_get_error_count(ivfpq_index* h, int64_t* out) {
       HIPCHECK(hipMemcpy(hdr, w.p_hdr.p, sizeof(hdr), hipMemcpyDeviceToHost));
       tot += hdr[15];
     }
+#ifdef DEVBUF_GUARD
+    {
+#define GCHK(buf, name)                                               \
+  if (!(buf).check_guard()) {                                         \
+    std::fprintf(stderr, "[guard] overwritten past %s\n", name);     \
+    tot += 1000000000;                                                \
+  }
+      GCHK(h->d_cent, "d_cent") GCHK(h->d_centT, "d_centT") GCHK(h->d_cnorm, "d_cnorm") GCHK(h->d_cb, "d_cb")
+      GCHK(h->d_T1, "d_T1") GCHK(h->d_codes, "d_codes") GCHK(h->d_ids, "d_ids") GCHK(h->d_off, "d_off")
+      GCHK(h->d_order, "d_order") GCHK(h->w_x, "w_x") GCHK(h->w_xn, "w_xn") GCHK(h->w_D, "w_D") GCHK(h->w_I, "w_I")
+      GCHK(h->w_lno, "w_lno") GCHK(h->w_codes, "w_codes") GCHK(h->w_cent, "w_cent") GCHK(h->w_cn, "w_cn")
+      GCHK(h->h_D, "h_D") GCHK(h->h_I, "h_I") GCHK(h->h_Iq, "h_Iq") GCHK(h->h_Dq, "h_Dq")
+      GCHK(h->q_lists, "q_lists") GCHK(h->q_ids, "q_ids") GCHK(h->q_codes, "q_codes") GCHK(h->a_off, "a_off")
+      for (auto& pt : h->pre) GCHK(pt.buf, "pre.buf")
+      for (auto& w : h->work) {
+        GCHK(w.w_dist, "w_dist") GCHK(w.w_lists, "w_lists") GCHK(w.w_dis0, "w_dis0") GCHK(w.w_T3, "w_T3")
+        GCHK(w.w_cand, "w_cand") GCHK(w.w_qn, "w_qn") GCHK(w.p_cnt, "p_cnt") GCHK(w.p_bucket, "p_bucket")
+        GCHK(w.p_recs, "p_recs") GCHK(w.p_hdr, "p_hdr") GCHK(w.p_D, "p_D") GCHK(w.p_I, "p_I") GCHK(w.p_N, "p_N")
+        GCHK(w.p_done, "p_done") GCHK(w.p_tau, "p_tau") GCHK(w.p_qmask, "p_qmask")
+      }
+#undef GCHK
+    }
+#endif
     *out = tot;
   });
 }

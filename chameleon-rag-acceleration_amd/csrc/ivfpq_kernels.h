@@ -93,6 +93,14 @@ void launch_pq_encode(const float* x, int64_t n, int d, const float* cent, const
 // one pair per query).  Work items are (list, up to G pairs of one kind); all
 // kind-0 items are scheduled before kind-1 items, so each query's running
 // k-th key (tau) is usually known when its other probes are scanned.
+// Stride of one per-wave partial list in partD / partI: k (-DPART_PAD=1, an A/B
+// variant of the batches-in-flight investigation: k > 64 rounded up to 32 entries so
+// that every list owns whole 128-B lines)
+#ifndef PART_PAD
+#define PART_PAD 0
+#endif
+inline int part_stride(int k) { return (PART_PAD && k > 64) ? (k + 31) & ~31 : k; }
+
 struct ListPlan {
   int32_t* cnt;      // [2][nloc] pair counts per kind; zero between batches (k_scan_lists re-zeroes)
   int2* bucket;      // [nloc][2 kinds][cap] (pair id q*nprobe+p, dis0 key bits)
@@ -116,6 +124,8 @@ struct ListPlan {
   int grid;          // persistent list-scan workgroups (multiple of 8)
   const int32_t* order = nullptr;  // [nloc] item order of the lists within a kind (nullable = list order)
   int fused = 0;     // 1: the list scan derives its items from cnt/bucket (no k_plan_items launch, recs unused)
+  int ks = 0;        // partial-list stride in entries (part_stride(k))
+  uint32_t* chk = nullptr;  // -DPART_CHECK experiment only: [nq][nprobe][4] (count, hash) of each partial list
 };
 
 struct ScanArgs {

@@ -1402,8 +1402,8 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
       for (int j = 0; j < p0 && use && !dup; j++) dup = lists[q * nprobe + j] == l;
       if (use && dup) {  // the merge reads every usable pair's partial slots: write them empty
         use = false;
-        const int64_t o = (q * nprobe + p) * 4 * (int64_t)k;
-        for (int e = 0; e < 4 * k; e++) {
+        const int64_t o = (q * nprobe + p) * 4 * (int64_t)pl.ks;
+        for (int e = 0; e < 4 * pl.ks; e++) {
           pl.partD[o + e] = FLT_MAX;
           pl.partI[o + e] = -1;
         }
@@ -1919,10 +1919,16 @@ __device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& p
 // A wave's sorted partial list of one pair into slot `slot` = pair * 4 + wave:
 // k <= 64 pads the list to k entries ((FLT_MAX, -1)); k > 64 writes the valid
 // entries and their count only (k_merge_big reads partN).
+#ifdef PART_CHECK
+__device__ __forceinline__ uint32_t part_hash(uint32_t kb, uint32_t pos, int ix) {
+  uint32_t h = kb * 0x9E3779B1u ^ (pos + 0x7F4A7C15u) * 0x85EBCA77u ^ (uint32_t)ix * 0xC2B2AE3Du;
+  return h ^ (h >> 15);
+}
+#endif
 template <int R>
 __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTopK<R>& tk, int64_t slot, int k,
                                               int64_t beg, int lane) {
-  const int64_t o = slot * k;
+  const int64_t o = slot * pl.ks;
   int n = 0;
 #pragma unroll
   for (int r = 0; r < R; r++) {
@@ -1936,6 +1942,49 @@ __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTo
   }
   if constexpr (R >= 2)
     if (lane == 0) pl.partN[slot] = n;
+#ifdef PART_CHECK
+  if constexpr (R >= 2) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int ix = r * 64 + lane;
+      if (ix < k && tk.p[r] != kKcNone)
+        h ^= part_hash(__float_as_uint(kc_key(tk.p[r])), (uint32_t)(beg + (int64_t)(uint32_t)tk.p[r]), ix);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) h ^= (uint32_t)__shfl_xor((int)h, off, 64);
+    if (lane == 0) {
+      pl.chk[4 * slot] = (uint32_t)n;
+      pl.chk[4 * slot + 1] = h;
+      atomicAdd(pl.chk + 4 * slot + 2, 1u);  // writes of this partial list in this batch
+    }
+    // read back what this wave just stored (L1 bypass): +100 when it differs already
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t hs = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int ix = r * 64 + lane;
+      if (ix < k && tk.p[r] != kKcNone) {
+        const uint32_t kb = __hip_atomic_load(reinterpret_cast<const uint32_t*>(pl.partD) + o + ix, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t pb = __hip_atomic_load(reinterpret_cast<const uint64_t*>(pl.partI) + o + ix, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        hs ^= part_hash(kb, (uint32_t)pb, ix);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) hs ^= (uint32_t)__shfl_xor((int)hs, off, 64);
+    if (lane == 0 && hs != h) atomicAdd(pl.err, 100);
+    // the written entries must be exactly indices 0 .. n - 1: +10000 per list with a hole
+    bool hole = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int ix = r * 64 + lane;
+      hole = hole || (ix < n && tk.p[r] == kKcNone);
+    }
+    if (__builtin_amdgcn_ballot_w64(hole) && lane == 0) atomicAdd(pl.err, 10000);
+  }
+#endif
 }
 
 // ROWK (k <= 16, G = 4, R = 1): the 4 pairs' running top-k share one 64-bit
@@ -2017,6 +2066,13 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     }
 #pragma unroll
     for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
+#ifdef PART_CHECK
+    // experiment: the bucket's pair must be a probe of this list (probe_list, written by
+    // the same coarse launch as the bucket); a mismatch adds 100000000
+    if (lane == 0)
+      for (int g = 0; g < G; g++)
+        if (g < it.cnt && a.probe_list[it.pair[g]] != (int64_t)it.l) atomicAdd(pl.err, 100000000);
+#endif
   };
 
   if (tid == 0) {
@@ -2462,7 +2518,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
       for (int g = 1; g < G; g++) pr = rg == g ? it.pair[g] : pr;
       if (rg < it.cnt && re < k) {
-        const int64_t o = ((int64_t)pr * 4 + wave) * k + re;
+        const int64_t o = ((int64_t)pr * 4 + wave) * pl.ks + re;
         const bool empty = rk == kKcNone;
         pl.partD[o] = empty ? FLT_MAX : kc_key(rk);
         pl.partI[o] = empty ? -1 : it.beg + (int64_t)(uint32_t)rk;
@@ -2484,6 +2540,14 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   }
 #ifdef SCAN_REL
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // A/B: coherence experiment
+#endif
+#ifdef ORDER_CANARY
+  // stream-order experiment: count this workgroup's exit once all its waves are done
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(pl.hdr + 13, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #endif
 }
 
@@ -2654,7 +2718,7 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
 #pragma unroll
       for (int g = 1; g < G; g++) pr = rg == g ? prev_pair[g] : pr;
       if (rg < prev_cnt && re < k) {
-        const int64_t o = ((int64_t)pr * 4 + wave) * k + re;
+        const int64_t o = ((int64_t)pr * 4 + wave) * pl.ks + re;
         const bool empty = q == kKcNone;
         pl.partD[o] = empty ? FLT_MAX : kc_key(q);
         pl.partI[o] = empty ? -1 : prev_beg + (int64_t)(uint32_t)q;
@@ -3051,6 +3115,9 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     const int nloc = a.list_hi - a.list_lo;
     for (int i = threadIdx.x; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
     if (threadIdx.x == 0) pl.hdr[2] = 0;
+#ifdef ORDER_CANARY
+    if (threadIdx.x == 0) pl.hdr[13] = 0;
+#endif
   }
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= a.nq) return;
@@ -3072,7 +3139,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     const int p = min(lane >> 2, np - 1);
     // the planner's mask of the probes the scan covered (empty or foreign lists are not)
     const bool scanned = (lane >> 2) < np && ((pl.qmask[q] >> p) & 1);
-    const int64_t base = ((q * np + p) * 4 + (lane & 3)) * k;
+    const int64_t base = ((q * np + p) * 4 + (lane & 3)) * pl.ks;
     // unconditional, clamped loads (no divergent branch around them); slots of
     // unscanned probes (empty or foreign lists, lanes past nprobe) were never
     // written this batch: their contents are stale and must not be used
@@ -3134,7 +3201,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   tk.init(k);
   const int L = 4 * np;
   const int total = L * k;
-  const int64_t qbase = q * (int64_t)total;
+  const int64_t qbase = q * (int64_t)L * pl.ks;
   for (int e0 = 0; e0 < total; e0 += 64 * B) {
     float d[B];
     int64_t pos[B];
@@ -3157,7 +3224,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
         }
         // k > 64 writes only each list's valid prefix (partN entries)
         if (scanned && (R == 1 || i < pl.partN[q * (int64_t)L + j])) {
-          const int64_t at = qbase + (int64_t)j * k + i;
+          const int64_t at = qbase + (int64_t)j * pl.ks + i;
           d[b] = pl.partD[at];
           pos[b] = pl.partI[at];
         }
@@ -3228,7 +3295,7 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   const int64_t qb = q * (int64_t)L;  // list j: entries at (qb + j) * k + i
   const float pad = a.ip ? -FLT_MAX : FLT_MAX;
   const float sgn = a.ip ? -1.f : 1.f;
-  auto key_at = [&](int j, int i) __attribute__((always_inline)) { return pl.partD[(qb + j) * k + i]; };
+  auto key_at = [&](int j, int i) __attribute__((always_inline)) { return pl.partD[(qb + j) * pl.ks + i]; };
 
   int C = 0;
 #pragma unroll
@@ -3338,7 +3405,7 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
           const int mid = (lo + hi) >> 1;
           if (sp[mid] <= e) lo = mid; else hi = mid;
         }
-        const int64_t at = (qb + lo) * k + (e - sp[lo]);
+        const int64_t at = (qb + lo) * pl.ks + (e - sp[lo]);
         cd[e] = pl.partD[at];
         cl[e] = pl.partI[at];
       }
@@ -3455,6 +3522,11 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
 #ifdef MERGE_ACQ
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // A/B: coherence experiment
 #endif
+#ifdef ORDER_CANARY
+  // every list-scan workgroup of this batch must have exited before this launch
+  if (threadIdx.x == 0 && __hip_atomic_load(pl.hdr + 13, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != pl.grid)
+    atomicAdd(pl.err, 1000);
+#endif
   __shared__ int s_len[256];
   __shared__ int s_hist[256];
   __shared__ int s_wsum[4];
@@ -3484,18 +3556,54 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     if (lane == 0) s_wsum[wave] = ws;
   }
   __syncthreads();
+#ifdef PART_CHECK
+  // experiment: each list as read here against (count, hash) as the scan wrote it;
+  // count mismatch -> +1000000, content mismatch -> +1000 in the error word
+  if (tid < L && ((qm >> (tid >> 2)) & 1)) {
+    const int64_t sl = qb + tid;
+    const uint32_t cn = __hip_atomic_load(pl.chk + 4 * sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ch = __hip_atomic_load(pl.chk + 4 * sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cw = __hip_atomic_load(pl.chk + 4 * sl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(pl.chk + 4 * sl + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cw != 1) atomicAdd(pl.err, 1000000);  // written by no item, or by more than one (as a count mismatch)
+    uint32_t h = 0;
+    for (int i = 0; i < s_len[tid]; i++)
+      h ^= part_hash(__float_as_uint(pl.partD[sl * pl.ks + i]), (uint32_t)pl.partI[sl * pl.ks + i], i);
+    if (cn != (uint32_t)s_len[tid]) {
+      atomicAdd(pl.err, 1000000);
+    } else if (h != ch) {
+      // re-read: agent-scope (L1 bypass) and system-scope loads; +100000 / +10000000 when
+      // those still differ from what the scan wrote
+      uint32_t h2 = 0, h3 = 0;
+      for (int i = 0; i < s_len[tid]; i++) {
+        const uint32_t kb = __hip_atomic_load(reinterpret_cast<const uint32_t*>(pl.partD) + sl * pl.ks + i,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t pb = __hip_atomic_load(reinterpret_cast<const uint64_t*>(pl.partI) + sl * pl.ks + i,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h2 ^= part_hash(kb, (uint32_t)pb, i);
+        const uint32_t kb3 = __hip_atomic_load(reinterpret_cast<const uint32_t*>(pl.partD) + sl * pl.ks + i,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t pb3 = __hip_atomic_load(reinterpret_cast<const uint64_t*>(pl.partI) + sl * pl.ks + i,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        h3 ^= part_hash(kb3, (uint32_t)pb3, i);
+      }
+      atomicAdd(pl.err, 1000 + (h2 != ch ? 100000 : 0) + (h3 != ch ? 10000000 : 0));
+    }
+  }
+#endif
   const int C = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-  const int E = L * k;
-  const float inv_k = 1.0f / (float)k;
-  const float* pd = pl.partD + qb * k;
+  const int ks = pl.ks;
+  const int E = L * ks;
+  const float inv_k = 1.0f / (float)ks;
+  const float* pd = pl.partD + qb * ks;
   uint32_t key[kRadixU];
 #pragma unroll
   for (int u = 0; u < kRadixU; u++) {
     const int e = u * 256 + tid;
     key[u] = 0xFFFFFFFFu;  // absent (no finite key maps here)
     if (e < E) {
-      const int j = div_small(e, k, inv_k);
-      if (e - j * k < s_len[j]) key[u] = ukey_of(pd[e]);
+      const int j = div_small(e, ks, inv_k);
+      if (e - j * ks < s_len[j]) key[u] = ukey_of(pd[e]);
     }
   }
   // the k-th smallest present key (all of them when there are at most k)
@@ -3545,7 +3653,7 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
   // compact the entries <= T (positions from partI)
   if (tid == 0) s_n = 0;
   __syncthreads();
-  const int64_t* pi = pl.partI + qb * k;
+  const int64_t* pi = pl.partI + qb * ks;
 #pragma unroll
   for (int u = 0; u < kRadixU; u++) {
     const bool c = key[u] <= T;  // (absent keys: 0xFFFFFFFF > T)
@@ -3970,7 +4078,7 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   }
   if (ev) (void)hipEventRecord(ev[1], s);
   if (R >= 2 && a.nprobe <= 64) {
-    if (MERGE_RADIX && 4 * a.nprobe * a.k <= kRadixU * 256)  // every key of a query in one workgroup's registers
+    if (MERGE_RADIX && 4 * a.nprobe * pl.ks <= kRadixU * 256)  // every key of a query in one workgroup's registers
       hipLaunchKernelGGL(k_merge_radix, dim3((unsigned)a.nq), dim3(256), 0, s, a, pl);
     else
       hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);

@@ -12,3 +12,6 @@ import json
 for l in open('$O/race2_$v.jsonl'):
     d=json.loads(l); print(d['k'], d['streams'], sum(r['bad_batches'] for r in d['per_round']), sum(r['err'] for r in d['per_round']))"
 done
+# kernel trace of the failing pattern (per-stream ordering of scan -> merges)
+RACE_ROUNDS=4 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/race2_trace -o run -- python3 -u profiles/race_diag.py 100,3 > $O/race2_trace.jsonl 2> $O/race2_trace.log || { echo "trace failed"; exit 1; }
+cat $O/race2_trace.jsonl

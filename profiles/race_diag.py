@@ -27,6 +27,9 @@ def main():
     configs = [(100, 3), (100, 2), (10, 3), (100, 4)]
     if len(sys.argv) > 1:
         configs = [tuple(int(v) for v in c.split(",")) for c in sys.argv[1:]]
+    # (k, streams[, hog]): hog = 1 keeps a 512 MB device-to-device copy loop running on
+    # a side stream (not the library's) while the batches run, with inflight off for
+    # a single stream -- memory latency under load without batch overlap
     rounds = int(os.environ.get("RACE_ROUNDS", "8"))
     xt = datasets.synthetic_sift_like(20_000, 64, seed=4321, n_centres=20_000)
     xb = datasets.synthetic_sift_like(100_000, 64, seed=1234, n_centres=20_000)
@@ -48,7 +51,12 @@ def main():
             ref.append((D.cpu().numpy(), I.cpu().numpy()))
         refs[k] = ref
     big = np.iinfo(np.int64).max
-    for k, nst in configs:
+    hog_a = torch.empty(1 << 27, device="cuda")
+    hog_b = torch.empty_like(hog_a)
+    side = torch.cuda.Stream()
+    for cfg in configs:
+        k, nst = cfg[0], cfg[1]
+        hog = len(cfg) > 2 and cfg[2] == 1
         t0 = time.time()
         streams = [torch.cuda.Stream() for _ in range(nst)]
         per_round = []
@@ -57,9 +65,13 @@ def main():
             e0 = ix.error_count()
             outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
                     for _ in range(nb)]
-            ix.inflight = True
+            ix.inflight = nst > 1
             try:
                 torch.cuda.synchronize()
+                if hog:
+                    with torch.cuda.stream(side):
+                        for _ in range(40):
+                            hog_b.copy_(hog_a)
                 for b in range(nb):
                     ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=streams[b % nst].cuda_stream)
                 torch.cuda.synchronize()
@@ -85,7 +97,7 @@ def main():
                                   "D": D[r, diff[:6]].tolist(), "D_ref": Dr[r, diff[:6]].tolist()}
             per_round.append({"bad_batches": bad_b, "bad_rows": bad_rows, "sentinels": sent, "nonfinite": nonfin,
                               "err": ix.error_count() - e0})
-        print(json.dumps({"k": k, "streams": nst, "rounds": rounds, "per_round": per_round, "first": detail,
+        print(json.dumps({"k": k, "streams": nst, "hog": hog, "rounds": rounds, "per_round": per_round, "first": detail,
                           "s": round(time.time() - t0, 1)}), flush=True)
 
 

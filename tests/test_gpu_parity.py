@@ -269,8 +269,9 @@ def test_batches_in_flight_on_round_robin_streams(rr_index, inflight):
     """24 batches issued round robin on 2, 3, 4 and 5 streams with no
     synchronisation, at k = 10 (row-packed scan) and k = 100 (k > 64 merge), with
     a coarse_device + preassigned search interleaved, in both stream modes:
-    searches ordered across streams, and batches in flight (up to three
-    overlapping in per-stream workspaces; 4 and 5 streams take workspaces over).
+    searches ordered across streams, and batches in flight (k = 10: up to three
+    overlapping in per-stream workspaces, 4 and 5 streams take workspaces over;
+    k = 100 searches are ordered in both modes, ivfpq_index.cpp kInflightMaxK).
     Every batch equals its search alone on one stream, bit for bit (those are
     checked against the oracle for the first batch), and the merge kernels'
     index checks count nothing."""
