@@ -825,10 +825,12 @@ struct ivfpq_index {
   bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
                      const ListPlan* plan = nullptr, float* T3out = nullptr) {
     if (nlist >= kSegmentedNlist && np <= 64) {  // large nlist: no [c][nlist] key matrix
-      W().w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist) * np);
+      W().w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist, d) * np);
+      W().w_qn.ensure(sizeof(float) * c);
       if (T3out) launch_ip_table(x, c, d, d_cb.as<float>(), M, ksub, T3out, s);
       launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, W().w_cand.as<uint64_t>(),
-                              dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
+                              dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>(),
+                              W().w_qn.as<float>());
       return plan != nullptr;
     }
     if (kFusedCoarse && coarse_fused_ok(nlist, d, np)) {  // keys in LDS, selection in the same launch

@@ -64,11 +64,13 @@ void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, 
 // centroid segment) the nprobe (<= 64) best (key, list) words on the matrix
 // cores (cand [nq][coarse_segments(nq, nlist)][nprobe]), then per query their
 // merge, output and (with plan) the batch planning of launch_coarse_select.
-int coarse_segments(int64_t nq, int nlist);
+// xn_buf (nullable, [nq] floats of scratch): with d % 4 == 0 and nq >= 64 the segments
+// are walked by 64-query tiles (k_coarse_segtop_tiled, |x|^2 from launch_row_norms).
+int coarse_segments(int64_t nq, int nlist, int d);
 void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                              int nprobe, uint64_t* cand, float* out_dis, int64_t* out_list, hipStream_t s, bool ip,
                              const ListPlan* plan = nullptr, const int64_t* list_off = nullptr, int lo = 0, int hi = 0,
-                             const float* cent = nullptr);
+                             const float* cent = nullptr, float* xn_buf = nullptr);
 
 // y[i][j] = sum_t x[i][t] * AT[t][j] (t-ordered fmaf chain) + b[j] (b nullable): OPQ / LinearTransform apply
 void launch_linear_transform(const float* x, int64_t n, int d_in, const float* AT, const float* b, int d_out, float* y,

@@ -919,6 +919,9 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
 // Faiss tree order as coarse_stage_queries).  Workgroups past the key tiles build
 // T3 as in k_coarse_gemm.
 constexpr int TQ = 64, TC = 128, TKC = 32;
+#ifndef TILED_SEGTOP
+#define TILED_SEGTOP 1  // -DTILED_SEGTOP=0: k_coarse_segtop (16-query tiles) for every segmented search (A/B)
+#endif
 constexpr int TAS = TKC + 2;   // A row stride (floats): 2 mod 32 -> conflict-free MFMA A reads
 constexpr int TBS = TC + 16;   // B row stride: 16 mod 32 -> conflict-free B reads
 
@@ -942,20 +945,14 @@ __device__ __forceinline__ void t3_role(const float* __restrict__ x, int64_t nq,
   }
 }
 
-__global__ __launch_bounds__(256) void k_coarse_gemm_tiled(const float* __restrict__ x, const float* __restrict__ xn,
-                                                           int64_t nq, int d, const float* __restrict__ centT,
-                                                           int ldc, const float* __restrict__ cn, int nlist,
-                                                           float* __restrict__ keys, int ip, int ngemm, CoarseT3 t3) {
-  __shared__ __attribute__((aligned(16))) float As[2][TQ * TAS];
-  __shared__ __attribute__((aligned(16))) float Bs[2][TKC * TBS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if ((int)blockIdx.x >= ngemm) {
-    t3_role(x, nq, d, t3, blockIdx.x - ngemm, &As[0][0], tid);
-    return;
-  }
-  const int nct = (nlist + TC - 1) / TC;
-  const int64_t q0 = (int64_t)(blockIdx.x / nct) * TQ;
-  const int c0 = (blockIdx.x % nct) * TC;
+// The wave's 16 queries x 128 centroids of a 64 x 128 tile (queries q0.., centroids
+// c0..), accumulated over d in ascending k: acc[t][r] = <x_{q0 + 16 wave + 4 k4 + r},
+// c_{c0 + 16 t + i16}>.  As / Bs are the double-buffered staging tiles; every wave
+// of the workgroup must call it (barriers), and they are free again on return.
+__device__ __forceinline__ void tiled_key_acc(f4 (&acc)[TC / 16], const float* __restrict__ x, int64_t q0, int64_t nq,
+                                              int d, const float* __restrict__ centT, int ldc, int c0,
+                                              float (*As)[TQ * TAS], float (*Bs)[TKC * TBS], int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
   // staging: thread t loads A row (t >> 2), k offsets 8 (t & 3) .. + 7 and B row (t >> 3),
   // columns 16 (t & 7) .. + 15; rows past nq / d and columns past nlist read as 0 / clamped
   const int ar = tid >> 2, ak = (tid & 3) * 8;
@@ -991,7 +988,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm_tiled(const float* __restri
     bq_[2] = rb2;                                                                                       \
     bq_[3] = rb3;                                                                                       \
   }
-  f4 acc[TC / 16];
 #pragma unroll
   for (int t = 0; t < TC / 16; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
   const int i16 = lane & 15, k4 = lane >> 4;
@@ -1017,6 +1013,25 @@ __global__ __launch_bounds__(256) void k_coarse_gemm_tiled(const float* __restri
   }
 #undef TILE_LOAD
 #undef TILE_STORE
+}
+
+__global__ __launch_bounds__(256) void k_coarse_gemm_tiled(const float* __restrict__ x, const float* __restrict__ xn,
+                                                           int64_t nq, int d, const float* __restrict__ centT,
+                                                           int ldc, const float* __restrict__ cn, int nlist,
+                                                           float* __restrict__ keys, int ip, int ngemm, CoarseT3 t3) {
+  __shared__ __attribute__((aligned(16))) float As[2][TQ * TAS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TKC * TBS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if ((int)blockIdx.x >= ngemm) {
+    t3_role(x, nq, d, t3, blockIdx.x - ngemm, &As[0][0], tid);
+    return;
+  }
+  const int nct = (nlist + TC - 1) / TC;
+  const int64_t q0 = (int64_t)(blockIdx.x / nct) * TQ;
+  const int c0 = (blockIdx.x % nct) * TC;
+  f4 acc[TC / 16];
+  tiled_key_acc(acc, x, q0, nq, d, centT, ldc, c0, As, Bs, tid);
+  const int i16 = lane & 15, k4 = lane >> 4;
 #pragma unroll
   for (int t = 0; t < TC / 16; t++) {
     const int c = c0 + t * 16 + i16;
@@ -3001,6 +3016,73 @@ __global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl
   }
 }
 
+// Segmented coarse quantizer on 64-query tiles (k_coarse_segtop's output from the
+// tiled key GEMM): workgroup = 64 queries x one segment of centroids, walked in
+// tiles of 128; each tile's keys go to LDS (in the staging buffers), and wave w keeps
+// the nprobe best (key, list) words of queries 16 w .. 16 w + 15 in packed one-row
+// top-k lists.  Each centroid column is read from L2 once per 64 queries (4x fewer
+// than k_coarse_segtop); the keys are k_coarse_gemm's to the bit.
+constexpr int TKS = TC + 1;  // key tile row stride (floats)
+static_assert(TQ * TKS <= 2 * TKC * TBS, "the key tile fits the B staging buffers");
+__global__ __launch_bounds__(256) void k_coarse_segtop_tiled(const float* __restrict__ x, const float* __restrict__ xn,
+                                                             int64_t nq, int d, const float* __restrict__ centT,
+                                                             int ldc, const float* __restrict__ cn, int nlist, int ip,
+                                                             int seg, int nseg, int nprobe,
+                                                             uint64_t* __restrict__ cand) {
+  __shared__ __attribute__((aligned(16))) float As[2][TQ * TAS];
+  __shared__ __attribute__((aligned(16))) float Bs[2][TKC * TBS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t q0 = (int64_t)(blockIdx.x / nseg) * TQ;
+  const int sg = blockIdx.x % nseg;
+  const int cb = sg * seg, ce = min(nlist, cb + seg);
+  const int i16 = lane & 15, k4 = lane >> 4;
+  float* kt = &Bs[0][0];  // [TQ][TKS] keys of the current tile
+  PackedTopK<1> tk[16];   // queries 16 wave .. 16 wave + 15
+#pragma unroll
+  for (int u = 0; u < 16; u++) tk[u].init(nprobe);
+  float xq[4];  // |x|^2 of this lane's 4 accumulator rows
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int64_t q = q0 + wave * 16 + k4 * 4 + r;
+    xq[r] = (ip || q >= nq) ? 0.f : xn[q];
+  }
+  for (int c0 = cb; c0 < ce; c0 += TC) {
+    f4 acc[TC / 16];
+    tiled_key_acc(acc, x, q0, nq, d, centT, ldc, c0, As, Bs, tid);
+#pragma unroll
+    for (int t = 0; t < TC / 16; t++) {
+      const int c = c0 + t * 16 + i16;
+      const float cnv = ip ? 0.f : cn[min(c, nlist - 1)];
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        kt[(wave * 16 + k4 * 4 + r) * TKS + t * 16 + i16] = coarse_key(acc[t][r], xq[r], cnv, ip);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const float* kr = kt + (wave * 16 + u) * TKS;
+#pragma unroll
+      for (int h = 0; h < TC / 64; h++) {
+        const int c = c0 + h * 64 + lane;
+        const uint64_t p = c < ce ? pack_kc(kr[h * 64 + lane], c) : kKcNone;
+        const bool pass = p < tk[u].tp;
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+        if (!mk) continue;  // wave-uniform
+        if (__popcll(mk) > 4)
+          kc_bulk_merge(tk[u], pass ? p : kKcNone, lane);
+        else
+          tk[u].insert(mk, p, lane);
+      }
+    }
+    __syncthreads();  // the keys are read before the next tile's staging overwrites them
+  }
+#pragma unroll
+  for (int u = 0; u < 16; u++) {
+    const int64_t q = q0 + wave * 16 + u;
+    if (q < nq && lane < nprobe) cand[(q * nseg + sg) * nprobe + lane] = tk[u].p[0];
+  }
+}
+
 // ------------------------------------------- large-nlist coarse (no key matrix)
 // Segmented coarse quantizer: workgroup = 16 queries x one segment of `seg`
 // centroids, walked in key tiles of 128 (coarse_key_tile: the MFMA keys of
@@ -3878,21 +3960,32 @@ void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, 
                      (nlist + 3) & ~3, cn, nlist, ip ? 1 : 0, nprobe, out_dis, out_list, (int)nkb, t3, cp);
 }
 
-int coarse_segments(int64_t nq, int nlist) {
-  const int64_t qt = (nq + GQ - 1) / GQ;
-  const int tiles = (nlist + GC - 1) / GC;
-  const int want = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (1024 + qt - 1) / qt));  // >= 1024 workgroups
+// the 64-query tiled form when the queries fill at least one tile and d % 4 == 0
+static bool segmented_tiled(int64_t nq, int d) { return TILED_SEGTOP && d % 4 == 0 && nq >= TQ; }
+
+int coarse_segments(int64_t nq, int nlist, int d) {
+  const bool tiled = segmented_tiled(nq, d);
+  const int64_t qt = tiled ? (nq + TQ - 1) / TQ : (nq + GQ - 1) / GQ;
+  const int tiles = (nlist + GC - 1) / GC;  // (TC == GC)
+  const int64_t min_wg = tiled ? 512 : 1024;  // two 54 KB workgroups per CU / four of k_coarse_segtop
+  const int want = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (min_wg + qt - 1) / qt));
   const int seg = (tiles + want - 1) / want * GC;
   return (nlist + seg - 1) / seg;
 }
 
 void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                              int nprobe, uint64_t* cand, float* out_dis, int64_t* out_list, hipStream_t s, bool ip,
-                             const ListPlan* plan, const int64_t* list_off, int lo, int hi, const float* cent) {
+                             const ListPlan* plan, const int64_t* list_off, int lo, int hi, const float* cent,
+                             float* xn_buf) {
   if (nq <= 0) return;
-  const int nseg = coarse_segments(nq, nlist);
+  const int nseg = coarse_segments(nq, nlist, d);
   const int tiles = (nlist + GC - 1) / GC;
   const int seg = (tiles + nseg - 1) / nseg * GC;
+  if (xn_buf && segmented_tiled(nq, d)) {
+    if (!ip) launch_row_norms(x, nq, d, xn_buf, s);
+    hipLaunchKernelGGL(k_coarse_segtop_tiled, dim3((unsigned)(nblocks(nq, TQ) * (unsigned)nseg)), dim3(256), 0, s, x,
+                       xn_buf, nq, d, centT, (nlist + 3) & ~3, cn, nlist, ip ? 1 : 0, seg, nseg, nprobe, cand);
+  } else {
   const int dk = (d + 63) & ~63;
   const size_t smem = sizeof(float) * ((size_t)dk * GQ + GQ + GQ * 8 + GQ * GC);
   if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device
@@ -3907,6 +4000,7 @@ void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* cen
   const unsigned grid = (unsigned)(nblocks(nq, GQ) * (unsigned)nseg);
   hipLaunchKernelGGL(k_coarse_segtop, dim3(grid), dim3(256), smem, s, x, nq, d, centT, (nlist + 3) & ~3, cn, nlist,
                      ip ? 1 : 0, seg, nseg, nprobe, cand);
+  }
   CoarsePlan cp;
   if (plan) {
     cp.pl = *plan;

@@ -249,23 +249,33 @@ def test_sliced_coarse_allgather_shards_c2(sift1m, nshards):
     assert_same(torch.cat(Dm).cpu().numpy(), torch.cat(Im).cpu().numpy(), Dr, Ir)
 
 
-@pytest.mark.parametrize("nq,nprobe", [(1, 1), (17, 33), (1000, 64)])
-def test_segmented_coarse_matches_oracle(nq, nprobe):
+@pytest.mark.parametrize("nq,nprobe,metric,gauss", [(1, 1, 1, 0), (17, 33, 1, 0), (1000, 64, 1, 0), (200, 32, 1, 1),
+                                                     (130, 16, 0, 1)])
+def test_segmented_coarse_matches_oracle(nq, nprobe, metric, gauss):
     """nlist >= 8192 takes the segmented coarse quantizer (per-segment top-nprobe
     on the matrix cores, no [nq][nlist] key matrix); nlist = 20000 leaves a
-    partial last tile, and the batch sizes give 1 to many segments per query."""
+    partial last tile, and the batch sizes give 1 to many segments per query.
+    From 64 queries on the segments are walked by 64-query tiles
+    (k_coarse_segtop_tiled); Gaussian data tests its rounding order, and the
+    inner-product case its IP keys."""
     import torch
 
     rng = np.random.default_rng(7)
     d, nlist, M = 96, 20000, 48
-    cent = rng.integers(0, 64, size=(nlist, d)).astype(np.float32)
+    if gauss:
+        cent = rng.standard_normal((nlist, d), dtype=np.float32)
+    else:
+        cent = rng.integers(0, 64, size=(nlist, d)).astype(np.float32)
     cent[123] = cent[456]  # an exact tie: ordered by list id
-    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, metric, device=0)
     ix.set_trained(cent, rng.standard_normal((M, 256, d // M), dtype=np.float32))
     ix.nprobe = nprobe
-    xq = rng.integers(0, 64, size=(nq, d)).astype(np.float32)
+    if gauss:
+        xq = rng.standard_normal((nq, d), dtype=np.float32)
+    else:
+        xq = rng.integers(0, 64, size=(nq, d)).astype(np.float32)
     Dq, Iq = ix.coarse_device(torch.from_numpy(xq).cuda())
-    Dr, Ir = O.coarse_search(xq, cent, nprobe)
+    Dr, Ir = O.coarse_search(xq, cent, nprobe, metric=metric)
     np.testing.assert_array_equal(Iq.cpu().numpy(), Ir)
     np.testing.assert_array_equal(Dq.cpu().numpy(), Dr)
 
