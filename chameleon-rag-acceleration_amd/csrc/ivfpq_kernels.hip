@@ -920,7 +920,7 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
 // T3 as in k_coarse_gemm.
 constexpr int TQ = 64, TC = 128, TKC = 32;
 #ifndef TILED_SEGTOP
-#define TILED_SEGTOP 1  // -DTILED_SEGTOP=0: k_coarse_segtop (16-query tiles) for every segmented search (A/B)
+#define TILED_SEGTOP 0  // -DTILED_SEGTOP=1: k_coarse_segtop_tiled (A/B: 512 vs 390 us per 1024 queries at C4, profiles/r04_ab.txt)
 #endif
 constexpr int TAS = TKC + 2;   // A row stride (floats): 2 mod 32 -> conflict-free MFMA A reads
 constexpr int TBS = TC + 16;   // B row stride: 16 mod 32 -> conflict-free B reads
