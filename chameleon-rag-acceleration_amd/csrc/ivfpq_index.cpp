@@ -240,6 +240,7 @@ struct ivfpq_index {
     DevBuf buf;
     int64_t n = 0;
     uint64_t seq = 0;  // the token; 0 = free
+    uint64_t freed_seq = 0;  // order in which free entries were consumed (reuse the longest-free one)
     hipEvent_t ready = nullptr;  // recorded after the table launch
     hipStream_t ready_stream = nullptr;
     hipEvent_t freed = nullptr;  // recorded after the consuming search's scans
@@ -879,6 +880,7 @@ struct ivfpq_index {
       require(pre[pi].n == n, "tables token was computed for " + std::to_string(pre[pi].n) + " queries, not " +
                                   std::to_string(n));
       pre[pi].seq = 0;
+      pre[pi].freed_seq = ++pre_seq;
     }
     const bool use_pre = pi >= 0;
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
@@ -969,7 +971,12 @@ struct ivfpq_index {
     int r = 0;
     for (int i = 1; i < kPreT3; i++) {
       const bool fi = pre[i].seq == 0, fr = pre[r].seq == 0;
-      if ((fi && !fr) || (fi == fr && pre[i].seq < pre[r].seq)) r = i;
+      // a free entry first, the one consumed longest ago (its consumer's scans are the
+      // likeliest to be done, so the wait below rarely stalls the side stream); else
+      // the oldest pending entry
+      if ((fi && !fr) || (fi && fr && pre[i].freed_seq < pre[r].freed_seq) ||
+          (!fi && !fr && pre[i].seq < pre[r].seq))
+        r = i;
     }
     PreT3& p = pre[r];
     if (p.freed_pending && p.freed_stream != s) HIPCHECK(hipStreamWaitEvent(s, p.freed, 0));
