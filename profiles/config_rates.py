@@ -63,6 +63,47 @@ def rate(ix, xq_dev, k, reps):
             "ms_per_batch_inflight2": ms2, "queries_per_s_inflight2": B / (ms2 * 1e-3)}
 
 
+def roofline(ix, xq_dev, k, M, steps=10):
+    """bench.py's roofline block for the list-scan kernel of this index: algorithmic code
+    bytes per batch (sum over queries and probes of the probed list's size x code size)
+    over the kernel's HIP-event duration (one batch at a time), and the stage split."""
+    import numpy as np
+    import torch
+
+    B = 1024
+    nb = xq_dev.shape[0] // B
+    sizes = ix.invlists.list_sizes()
+    alg = []
+    for b in range(nb):
+        _, Iq = ix.coarse_device(xq_dev[b * B:(b + 1) * B])
+        Iq = Iq.cpu().numpy()
+        alg.append(int(np.where(Iq >= 0, sizes[np.maximum(Iq, 0)], 0).sum()) * M)
+    D = torch.empty((B, k), dtype=torch.float32, device=xq_dev.device)
+    I = torch.empty((B, k), dtype=torch.int64, device=xq_dev.device)
+    ix.search_device(xq_dev[:B], k, D, I)
+    torch.cuda.synchronize()
+    ix.set_timing(True, lists_only=True)
+    for s in range(steps):
+        b = s % nb
+        ix.search_device(xq_dev[b * B:(b + 1) * B], k, D, I)
+    torch.cuda.synchronize()
+    ix.set_timing(False)
+    ms, n = ix.get_timing()["lists"]
+    avg = ms / max(n, 1)
+    bpl = sum(alg[s % nb] for s in range(steps)) / steps
+    ix.set_timing(True)
+    for s in range(steps):
+        b = s % nb
+        ix.search_device(xq_dev[b * B:(b + 1) * B], k, D, I)
+    torch.cuda.synchronize()
+    ix.set_timing(False)
+    split = {st: v[0] / max(v[1], 1) for st, v in ix.get_timing().items()}
+    ach = bpl / (avg * 1e-3) / 1e9
+    return {"roofline": {"bound": "hbm", "kernel": "k_scan_lists", "alg_bytes_per_launch": bpl, "avg_launch_ms": avg,
+                         "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0},
+            "stages_ms": split}
+
+
 def embed_like(x, mu):
     """Centred, unit-norm rows (sentence-embedding-like): inner-product k-means on the raw
     non-negative synthetic data would put almost every vector in a few lists."""
@@ -109,6 +150,7 @@ def main():
         xq = torch.from_numpy(datasets.synthetic_sift_like(10240, 128, seed=123)).cuda()
         ix.nprobe = 8
         r = rate(ix, xq, 10, a.reps)
+        r.update(roofline(ix, xq, 10, 16))
         print(json.dumps({"config": "C1 shape on GPU: SIFT1M-shaped IVF1024,PQ16 nprobe 8", **r,
                           "setup_s": time.time() - t0}), flush=True)
         del ix, xq
@@ -135,6 +177,7 @@ def main():
         ix.nprobe = 32
         for k in (10, 1000):
             r = rate(ix, xq, k, a.reps)
+            r.update(roofline(ix, xq, k, 64))
             print(json.dumps({"config": f"C3 shape: d 768, nb {ix.ntotal}, IVF4096,PQ64, nprobe 32, inner product",
                               **r, "setup_s": time.time() - t0}), flush=True)
         del ix, xq
@@ -144,6 +187,7 @@ def main():
         xq = torch.from_numpy(datasets.synthetic_sift_like(4096, 96, seed=123, n_centres=200000)).cuda()
         ix.nprobe = 32
         r = rate(ix, xq, 10, a.reps)
+        r.update(roofline(ix, xq, 10, 48))
         print(json.dumps({"config": f"C4 shape, one shard: d 96, nb {ix.ntotal}, IVF65536,PQ48, nprobe 32", **r,
                           "setup_s": time.time() - t0}), flush=True)
 
