@@ -1092,6 +1092,40 @@ __global__ __launch_bounds__(256) void k_t3_mfma(const float* __restrict__ x, in
 
 // Write a query's top-nprobe (run: packed (key, list), ascending across the
 // wave) and, with cp.on, plan its probes for the list-major scan.
+// -<x_q, c_{l(p)}> in Faiss tree order (tree<K_IP> over d) for the probes p < np of one
+// query, probe p's list given by lane p's `l` (l < 0: not needed, any value returned):
+// eight lanes per probe, lane j of a group holding the tree's accumulator j (as
+// k_row_norms), so a 768-d product is 96 dependent steps per lane instead of 768 in
+// one.  Must be called by the whole wave; the result is returned in lane p.
+__device__ __forceinline__ float wave_ip_dis0(const float* __restrict__ xq, const float* __restrict__ cent, int64_t l,
+                                             int d, int np, int lane) {
+  const int j = lane & 7;
+  const int d8 = d & ~7;
+  float res = 0.f;
+  for (int pass = 0; pass * 8 < np; pass++) {  // wave-uniform
+    const int pp = pass * 8 + (lane >> 3);
+    const int64_t lp = (int64_t)(((uint64_t)(uint32_t)__shfl((int)((uint64_t)l >> 32), pp & 63) << 32) |
+                                 (uint32_t)__shfl((int)(uint32_t)(uint64_t)l, pp & 63));
+    const bool ok = pp < np && lp >= 0;
+    const float* cl = cent + (ok ? lp : 0) * d;
+    float a = 0.f;
+    if (ok)
+      for (int t = j; t < d8; t += 8) a = a + xq[t] * cl[t];
+    float a4 = __shfl_down(a, 4, 8) + a;  // a8[j + 4] + a8[j]
+    int r = d8;
+    if (r + 4 <= d) {
+      if (ok && j < 4) a4 = a4 + xq[r + j] * cl[r + j];
+      r += 4;
+    }
+    if (ok && j < 4 && r + j < d) a4 = a4 + xq[r + j] * cl[r + j];
+    const float h = a4 + __shfl_down(a4, 1, 8);
+    const float v = h + __shfl_down(h, 2, 8);  // lane 8 g: probe pass * 8 + g
+    const float mine = __shfl(v, (lane & 7) * 8);
+    if ((lane >> 3) == pass) res = mine;
+  }
+  return -res;
+}
+
 __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, int nprobe, float* __restrict__ out_dis,
                                             int64_t* __restrict__ out_list, int ip, const float* __restrict__ x, int d,
                                             const CoarsePlan& cp) {
@@ -1108,15 +1142,9 @@ __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, i
     const uint64_t um = __ballot(use);
     const int fp = um ? (int)__builtin_ctzll(um) : 64;
     if (lane == 0) cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
-    if (use) {
-      float d0 = rd;
-      if (ip) {
-        const float* xq = x + q * d;
-        const float* cl = cp.cent + l * d;
-        d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
-      }
-      plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
-    }
+    float d0 = rd;
+    if (ip && um) d0 = wave_ip_dis0(x + q * d, cp.cent, use ? l : -1, d, nprobe, lane);  // (wave-uniform)
+    if (use) plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
   }
 }
 
@@ -1344,6 +1372,36 @@ __global__ __launch_bounds__(256) void k_ip_table(const float* __restrict__ x, i
   }
 }
 
+// T3 by (16 queries, sub-quantizer m) tiles: thread t holds codeword (m, t) in
+// registers (read once per 16 queries instead of once per query: C3's codebook is
+// 786 KB, which k_ip_table read from L2 for every query) and writes entry
+// (q, m, t) for the 16 queries, coalesced over t.  Same tree order as k_ip_table.
+template <int DSUB>
+__global__ __launch_bounds__(256) void k_ip_tiles(const float* __restrict__ x, int64_t n, int d,
+                                                  const float* __restrict__ cb, int M, float* __restrict__ out) {
+  __shared__ float xs[GQ * DSUB];
+  const int tid = threadIdx.x;
+  const int64_t q0 = (int64_t)(blockIdx.x / M) * GQ;
+  const int m = blockIdx.x % M;
+  for (int i = tid; i < GQ * DSUB; i += 256) {
+    const int qq = i / DSUB;
+    xs[i] = q0 + qq < n ? x[(q0 + qq) * d + m * DSUB + (i - qq * DSUB)] : 0.f;
+  }
+  float cw[DSUB];
+  const float* src = cb + ((int64_t)m * 256 + tid) * DSUB;
+#pragma unroll
+  for (int t = 0; t < DSUB; t++) cw[t] = src[t];
+  __syncthreads();
+  const int total = M * 256;
+  const int nqq = (int)min<int64_t>(GQ, n - q0);
+#pragma unroll 4
+  for (int qq = 0; qq < nqq; qq++) {
+    const float* xq = xs + qq * DSUB;
+    out[(q0 + qq) * total + m * 256 + tid] =
+        tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cw[t]; }, DSUB);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_precompute_T1(const float* __restrict__ cent, int nlist, int d,
                                                        const float* __restrict__ cb, int M, int ksub,
                                                        float* __restrict__ T1) {
@@ -1429,15 +1487,10 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
     const int fp = (!found && um) ? (int)__builtin_ctzll(um) : 64;
     found = found || um != 0;
     if (p0 == 0 && lane == 0) pl.qmask[q] = um;  // (nprobe <= 64 only: the merge reads it then)
+    float d0 = 0.f;
+    if (ip && um) d0 = wave_ip_dis0(x + q * d, cent, use ? l : -1, d, min(64, nprobe - p0), lane);  // (uniform)
     if (use) {
-      float d0;
-      if (ip) {
-        const float* xq = x + q * d;
-        const float* cl = cent + l * d;
-        d0 = -tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cl[t]; }, d);
-      } else {
-        d0 = Dq ? Dq[q * nprobe + p] : 0.f;
-      }
+      if (!ip) d0 = Dq ? Dq[q * nprobe + p] : 0.f;
       plan_pair(pl, hi - lo, l, lo, lane == fp ? 0 : 1, (int)(q * nprobe + p), d0);
     }
   }
@@ -3877,17 +3930,11 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
   if (xn_buf && coarse_tiled_ok(d, nq)) {  // large d: 64-query x 128-centroid tiles, k-chunks staged in LDS
     if (!ip) launch_row_norms(x, nq, d, xn_buf, s);
     const int ngemm = (int)(nblocks(nq, TQ) * nblocks(nlist, TC));
-    CoarseT3 t3;
-    if (T3out && M > 0 && d % M == 0 && d / M <= 2 * TQ * TAS / GQ) {
-      t3.out = T3out;
-      t3.cb = cb;
-      t3.M = M;
-      t3.nblk = (int)(nblocks(nq, GQ) * (unsigned)M);
-    } else if (T3out) {
-      launch_ip_table(x, nq, d, cb, M, 256, T3out, s);
-    }
-    hipLaunchKernelGGL(k_coarse_gemm_tiled, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), 0, s, x, xn_buf, nq, d,
-                       centT, (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
+    // T3 in its own launch: as extra workgroups of this kernel each would hold the
+    // GEMM's 54 KB of static LDS, two per CU (C3: 4 096 T3 workgroups, ~0.13 ms)
+    if (T3out) launch_ip_table(x, nq, d, cb, M, 256, T3out, s);
+    hipLaunchKernelGGL(k_coarse_gemm_tiled, dim3((unsigned)ngemm), dim3(256), 0, s, x, xn_buf, nq, d, centT,
+                       (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, CoarseT3{});
     return;
   }
   const unsigned nqb = nblocks(nq, GQ);
@@ -4043,6 +4090,17 @@ void launch_ip_table(const float* x, int64_t n, int d, const float* cb, int M, i
   const int dsub = d / M;
   const dim3 grid((unsigned)n);
   if (d > 2048 || (M * ksub) % 16 != 0) return;  // guarded by the host (d <= 2048, ksub = 256)
+  if (ksub == 256 && n >= GQ) {  // (16 queries, m) tiles: the codebook read once per 16 queries
+    const dim3 tg((unsigned)(nblocks(n, GQ) * (unsigned)M));
+    switch (dsub) {
+      case 2: hipLaunchKernelGGL(k_ip_tiles<2>, tg, dim3(256), 0, s, x, n, d, cb, M, out); return;
+      case 4: hipLaunchKernelGGL(k_ip_tiles<4>, tg, dim3(256), 0, s, x, n, d, cb, M, out); return;
+      case 8: hipLaunchKernelGGL(k_ip_tiles<8>, tg, dim3(256), 0, s, x, n, d, cb, M, out); return;
+      case 12: hipLaunchKernelGGL(k_ip_tiles<12>, tg, dim3(256), 0, s, x, n, d, cb, M, out); return;
+      case 16: hipLaunchKernelGGL(k_ip_tiles<16>, tg, dim3(256), 0, s, x, n, d, cb, M, out); return;
+      default: break;
+    }
+  }
   switch (dsub) {
     case 2: hipLaunchKernelGGL(k_ip_table<2>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
     case 4: hipLaunchKernelGGL(k_ip_table<4>, grid, dim3(256), 0, s, x, n, d, cb, M, ksub, out); break;
