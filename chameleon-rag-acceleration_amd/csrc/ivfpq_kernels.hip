@@ -1109,8 +1109,20 @@ __device__ __forceinline__ float wave_ip_dis0(const float* __restrict__ xq, cons
     const bool ok = pp < np && lp >= 0;
     const float* cl = cent + (ok ? lp : 0) * d;
     float a = 0.f;
-    if (ok)
-      for (int t = j; t < d8; t += 8) a = a + xq[t] * cl[t];
+    if (ok) {
+      int t = j;
+      for (; t + 56 < d8; t += 64) {  // eight loads of each operand in flight, adds in element order
+        float xv[8], cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          xv[u] = xq[t + 8 * u];
+          cv[u] = cl[t + 8 * u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) a = a + xv[u] * cv[u];
+      }
+      for (; t < d8; t += 8) a = a + xq[t] * cl[t];
+    }
     float a4 = __shfl_down(a, 4, 8) + a;  // a8[j + 4] + a8[j]
     int r = d8;
     if (r + 4 <= d) {
