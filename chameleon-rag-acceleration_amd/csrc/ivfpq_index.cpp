@@ -198,7 +198,10 @@ constexpr bool kTiledCoarse = TILED_COARSE;
 // returned wrong rows in about 1 batch of 40 when two of them overlapped, and the
 // cause is not found (profiles/r04_race.txt): they are ordered after
 // every search in flight, in either mode.
-constexpr int kInflightMaxK = 64;
+#ifndef INFLIGHT_MAXK
+#define INFLIGHT_MAXK 64  // experiments: -DINFLIGHT_MAXK=1024 lets every k overlap
+#endif
+constexpr int kInflightMaxK = INFLIGHT_MAXK;
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on

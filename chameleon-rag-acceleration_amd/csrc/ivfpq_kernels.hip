@@ -2008,6 +2008,9 @@ __device__ __forceinline__ uint32_t part_hash(uint32_t kb, uint32_t pos, int ix)
 template <int R>
 __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTopK<R>& tk, int64_t slot, int k,
                                               int64_t beg, int lane) {
+#if defined(WAIT_AT) && WAIT_AT == 1  // experiment: every memory result waited for before the partial writes
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
   const int64_t o = slot * pl.ks;
   int n = 0;
 #pragma unroll
@@ -2022,6 +2025,9 @@ __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTo
   }
   if constexpr (R >= 2)
     if (lane == 0) pl.partN[slot] = n;
+#if defined(WAIT_AT) && WAIT_AT == 2  // experiment: ... after them
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
 #ifdef PART_CHECK
   if constexpr (R >= 2) {
     uint32_t h = 0;
@@ -2346,6 +2352,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       }
 #pragma unroll
       for (int g = 0; g < G; g++) qn[g] = 0;
+#if defined(WAIT_AT) && WAIT_AT == 3  // experiment: ... at the end of every queue drain
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
       loose = false;
 #pragma unroll
       for (int g = 0; g < G; g++) {
