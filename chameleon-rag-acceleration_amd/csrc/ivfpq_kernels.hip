@@ -817,11 +817,16 @@ __device__ __forceinline__ void coarse_key_tile(f4 (&acc)[NT], const float* xs, 
     }
   };
   constexpr int CH = 4 * KS;  // k per chunk
+  // chunks up to the first multiple of CH at or past d (the staged A rows are zero up to
+  // dk >= kend; an all-zero chunk would leave every accumulator unchanged): d = 96 takes
+  // 3 chunks, not the 4 of its 64-padded staging
+  const int kend = min(dk, (d + CH - 1) / CH * CH);
   load_b(0, b0);
-  for (int k0 = 0; k0 < dk; k0 += 2 * CH) {
-    load_b(k0 + CH, b1);
+  for (int k0 = 0; k0 < kend; k0 += 2 * CH) {
+    load_b(k0 + CH, b1);  // past the end on the last pass: clamped, unused
     mma(k0, b0);
-    load_b(k0 + 2 * CH, b0);  // past the end on the last pass: clamped, unused
+    if (k0 + CH >= kend) break;
+    load_b(k0 + 2 * CH, b0);
     mma(k0 + CH, b1);
   }
 }
@@ -3166,6 +3171,7 @@ __global__ __launch_bounds__(256) void k_coarse_segtop_tiled(const float* __rest
 // few, bulk-merged when many.  Output: cand [nq][nseg][nprobe] packed words
 // (kKcNone = none).  The [nq][nlist] key matrix is never written (C4: 1024 x
 // 65536 keys would be 256 MB per chunk).
+constexpr int kSegQ = 128;  // candidate queue per query (k_coarse_segtop)
 __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__ x, int64_t nq, int d,
                                                        const float* __restrict__ centT, int ldc,
                                                        const float* __restrict__ cn, int nlist, int ip, int seg,
@@ -3181,14 +3187,36 @@ __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__
   float* xs = g_lds;             // [dk][GQ]
   float* xn = xs + dk * GQ;      // [GQ] + 128 scratch
   float* kt = xn + GQ + GQ * 8;  // [GQ][GC] key tile
+  // per query a queue of candidate words under its running nprobe-th, merged 64 at a
+  // time (kSegQ per query): a tile's survivors are appended, not merged one tile at a time
+  uint64_t* cq = reinterpret_cast<uint64_t*>(kt + GQ * GC);
   coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
   const int i16 = lane & 15, k4 = lane >> 4;
+  const uint64_t lt = (1ull << lane) - 1;
   PackedTopK<1> tk[4];  // queries 4 wave .. 4 wave + 3
+  int qn[4];            // queue fills (wave-uniform)
 #pragma unroll
-  for (int u = 0; u < 4; u++) tk[u].init(nprobe);
+  for (int u = 0; u < 4; u++) {
+    tk[u].init(nprobe);
+    qn[u] = 0;
+  }
+  auto drain = [&](int u) __attribute__((always_inline)) {
+    uint64_t* qv = cq + (wave * 4 + u) * kSegQ;
+    for (int b = 0; b < qn[u]; b += 64) {
+      uint64_t c = b + lane < qn[u] ? qv[b + lane] : kKcNone;
+      c = c < tk[u].tp ? c : kKcNone;
+      if (__builtin_amdgcn_ballot_w64(c != kKcNone)) kc_bulk_merge(tk[u], c, lane);
+    }
+    qn[u] = 0;
+  };
   for (int t0 = cb; t0 < ce; t0 += GC) {
     f4 acc[NTL];
+#ifdef SEGTOP_NOMMA  // timing experiment only (wrong results): no key tiles
+#pragma unroll
+    for (int t = 0; t < NTL; t++) acc[t] = f4{(float)t0, 1.f, 2.f, 3.f};
+#else
     coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, t0 + wave * 32, lane);
+#endif
     __syncthreads();  // xn (first tile); the previous tile's keys have been read
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
@@ -3201,6 +3229,9 @@ __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__
       }
     }
     __syncthreads();
+#ifdef SEGTOP_NOSEL  // timing experiment only (wrong results): no selection
+    if (t0 >= 0) continue;
+#endif
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int i = wave * 4 + u;
@@ -3211,15 +3242,16 @@ __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__
         const bool pass = p < tk[u].tp;
         const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
         if (!mk) continue;  // wave-uniform
-        if (__popcll(mk) > 4)
-          kc_bulk_merge(tk[u], pass ? p : kKcNone, lane);
-        else
-          tk[u].insert(mk, p, lane);
+        const int cnt = (int)__popcll(mk);
+        if (qn[u] + cnt > kSegQ) drain(u);
+        if (pass) cq[i * kSegQ + qn[u] + (int)__popcll(mk & lt)] = p;
+        qn[u] += cnt;
       }
     }
   }
 #pragma unroll
   for (int u = 0; u < 4; u++) {
+    drain(u);
     const int64_t q = q0 + wave * 4 + u;
     if (q < nq && lane < nprobe) cand[(q * nseg + sg) * nprobe + lane] = tk[u].p[0];
   }
@@ -4055,7 +4087,7 @@ void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* cen
                        xn_buf, nq, d, centT, (nlist + 3) & ~3, cn, nlist, ip ? 1 : 0, seg, nseg, nprobe, cand);
   } else {
   const int dk = (d + 63) & ~63;
-  const size_t smem = sizeof(float) * ((size_t)dk * GQ + GQ + GQ * 8 + GQ * GC);
+  const size_t smem = sizeof(float) * ((size_t)dk * GQ + GQ + GQ * 8 + GQ * GC) + sizeof(uint64_t) * GQ * kSegQ;
   if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device
     static uint64_t attr_done = 0;
     int dev = 0;
