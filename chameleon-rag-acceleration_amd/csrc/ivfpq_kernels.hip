@@ -4262,7 +4262,10 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   constexpr int G = scan_group(M, R);
   // code chunks held in registers per item (32 VGPRs), even; r02 A/B at C2 M = 16:
   // 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
-  constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : 2;
+#ifndef JB_WIDE
+#define JB_WIDE 4  // code chunks in registers per item at M > 32 (r04 A/B vs 2: C3 scan 643 -> 624 us, C4 214 -> 210 us)
+#endif
+  constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : JB_WIDE;
   if (ev) (void)hipEventRecord(ev[0], s);
   if constexpr (G == 4 && R == 1 && M <= 16 && SCAN_PIPE) {
     if (a.k <= 16 && pl.fused) {  // one workgroup per CU
