@@ -16,6 +16,9 @@
 //   mode 4: W holds its workgroups ~50 us after its stores (dirty lines stay in L2
 //           while the other streams' kernels start and end)
 //   mode 5: as 4, with agent-scope (sc1, write-through) stores in W
+//   mode 6: R pinned by XCD: a reader workgroup on XCD x reads chunks x, x + 8, ... (its
+//           XCC_ID hardware register), so every chunk is read on the same XCD every
+//           iteration and a line that XCD's L2 kept from the previous read would be hit
 //   partial = 1: W writes only the first 40 of every 128 bytes (the rest keeps the
 //               previous iteration's values; R checks only those 40 bytes)
 // Prints one JSON line: mismatching words per stream.
@@ -61,7 +64,11 @@ __global__ __launch_bounds__(256) void k_write(unsigned* b, unsigned it, int mod
 __global__ __launch_bounds__(256) void k_read(const unsigned* b, unsigned it, int mode, int partial, unsigned* err) {
   if (mode == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (mode == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  const unsigned chunk = (blockIdx.x * 37u + 11u) % kBlocks;  // another workgroup's chunk
+  unsigned chunk = (blockIdx.x * 37u + 11u) % kBlocks;  // another workgroup's chunk
+  if (mode == 6) {
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11)) & 7u;  // HW_REG_XCC_ID[3:0]
+    chunk = (xcc + 8u * (blockIdx.x / 8u)) % kBlocks;
+  }
   const unsigned base = chunk * 1024u;
   unsigned bad = 0;
   for (unsigned t = threadIdx.x; t < 1024u; t += 256u) {
