@@ -2023,13 +2023,26 @@ __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTo
     const int ix = r * 64 + lane;
     const bool empty = tk.p[r] == kKcNone;
     if (ix < k && (R == 1 || !empty)) {
+#ifdef PART_WT  // experiment: write-through (agent-scope) partial stores
+      __hip_atomic_store(pl.partD + o + ix, empty ? FLT_MAX : kc_key(tk.p[r]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(pl.partI + o + ix, empty ? (int64_t)-1 : beg + (int64_t)(uint32_t)tk.p[r], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+#else
       pl.partD[o + ix] = empty ? FLT_MAX : kc_key(tk.p[r]);
       pl.partI[o + ix] = empty ? -1 : beg + (int64_t)(uint32_t)tk.p[r];  // global code position
+#endif
     }
     if constexpr (R >= 2) n += __popcll(__builtin_amdgcn_ballot_w64(ix < k && !empty));
   }
   if constexpr (R >= 2)
-    if (lane == 0) pl.partN[slot] = n;
+    if (lane == 0) {
+#ifdef PART_WT
+      __hip_atomic_store(pl.partN + slot, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+      pl.partN[slot] = n;
+#endif
+    }
 #if defined(WAIT_AT) && WAIT_AT == 2  // experiment: ... after them
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif
