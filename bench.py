@@ -91,10 +91,11 @@ def parse():
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=1,
                    help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 turns the "
                         "index's batches-in-flight mode on so that consecutive batches overlap, DESIGN.md "
-                        "section 4); 1 = one batch at a time on one stream")
+                        "section 4 -- experimental: ~1e-4 of overlapped batches differ from the oracle); "
+                        "1 = one batch at a time on one stream (the parity-clean path, default)")
     return p.parse_args()
 
 
@@ -254,8 +255,26 @@ def main():
         for s in range(n_ex):
             ix.search(xq_host[s % args.nbatches], k)
         extra["host_search_queries_per_s"] = n_ex * Bg / (time.perf_counter() - t0)
+        if inflight == 1:  # the experimental overlap mode, two streams, reported beside the value only
+            st2 = [torch.cuda.Stream(dev) for _ in range(2)]
+            D2 = [torch.empty_like(Dbuf) for _ in range(2)]
+            I2 = [torch.empty_like(Ibuf) for _ in range(2)]
+            ix.inflight = True
+            try:
+                for j in range(2):
+                    ix.search_device(xq_dev[j % args.nbatches], k, D2[j], I2[j], stream=st2[j].cuda_stream)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for s in range(args.steps):
+                    ix.search_device(xq_dev[s % args.nbatches], k, D2[s % 2], I2[s % 2], stream=st2[s % 2].cuda_stream)
+                torch.cuda.synchronize()
+                extra["overlap2_queries_per_s_experimental"] = args.steps * Bg / (time.perf_counter() - t0)
+            finally:
+                ix.inflight = False
         extra["note"] = (f"{n_ex} batches each; k100 = search_device with k=100 (one stream: k > 64 searches "
-                         f"are not overlapped); "
+                         f"are not overlapped); overlap2 = {args.steps} steps with two batches in flight on two "
+                         f"streams (experimental, not the value: 2 in 24000 such batches differed from the "
+                         f"oracle, profiles/r04_race_rate.jsonl); "
                          f"host_search = search() on numpy "
                          f"queries (H2D copy, search, D2H copy; synchronous)")
     if world > 1:

@@ -29,7 +29,8 @@ def main():
         configs = [tuple(int(v) for v in c.split(",")) for c in sys.argv[1:]]
     # (k, streams[, hog]): hog = 1 keeps a 512 MB device-to-device copy loop running on
     # a side stream (not the library's) while the batches run, with inflight off for
-    # a single stream -- memory latency under load without batch overlap
+    # a single stream -- memory latency under load without batch overlap; hog = 2: a
+    # coarse_device + preassigned search on batch 5's stream before it (the test's mix)
     rounds = int(os.environ.get("RACE_ROUNDS", "8"))
     xt = datasets.synthetic_sift_like(20_000, 64, seed=4321, n_centres=20_000)
     xb = datasets.synthetic_sift_like(100_000, 64, seed=1234, n_centres=20_000)
@@ -57,6 +58,7 @@ def main():
     for cfg in configs:
         k, nst = cfg[0], cfg[1]
         hog = len(cfg) > 2 and cfg[2] == 1
+        mix = len(cfg) > 2 and cfg[2] == 2
         t0 = time.time()
         streams = [torch.cuda.Stream() for _ in range(nst)]
         per_round = []
@@ -65,7 +67,7 @@ def main():
             e0 = ix.error_count()
             outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
                     for _ in range(nb)]
-            ix.inflight = nst > 1
+            ix.inflight = nst > 1 and os.environ.get("RACE_INFLIGHT", "1") != "0"
             try:
                 torch.cuda.synchronize()
                 if hog:
@@ -73,7 +75,12 @@ def main():
                         for _ in range(40):
                             hog_b.copy_(hog_a)
                 for b in range(nb):
-                    ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=streams[b % nst].cuda_stream)
+                    st = streams[b % nst]
+                    if mix and b == 5:
+                        with torch.cuda.stream(st):
+                            Dq, Iq = ix.coarse_device(xd[b], stream=st.cuda_stream)
+                            ix.search_preassigned_device(xd[b], k, Iq, Dq, stream=st.cuda_stream)
+                    ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=st.cuda_stream)
                 torch.cuda.synchronize()
             finally:
                 ix.inflight = False
@@ -97,7 +104,9 @@ def main():
                                   "D": D[r, diff[:6]].tolist(), "D_ref": Dr[r, diff[:6]].tolist()}
             per_round.append({"bad_batches": bad_b, "bad_rows": bad_rows, "sentinels": sent, "nonfinite": nonfin,
                               "err": ix.error_count() - e0})
-        print(json.dumps({"k": k, "streams": nst, "hog": hog, "rounds": rounds, "per_round": per_round, "first": detail,
+        print(json.dumps({"k": k, "streams": nst, "hog": hog, "mix": mix, "rounds": rounds,
+                          "bad_batches": sum(r["bad_batches"] for r in per_round),
+                          "bad_rounds": [dict(r, round=i) for i, r in enumerate(per_round) if r["bad_batches"] or r["err"]], "first": detail,
                           "s": round(time.time() - t0, 1)}), flush=True)
 
 
