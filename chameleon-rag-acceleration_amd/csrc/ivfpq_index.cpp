@@ -29,6 +29,50 @@
 #include "ivfpq_build.h"
 
 using namespace chivf;
+#ifdef WZ_BISECT
+// experiment (profiles/build_wz_bisect.sh): the launchers of a forcezero build of the
+// kernels, chosen per search stage by IVFPQ_WZ = coarse | scan | merge
+namespace chivf {
+void set_launch_parts(int p);
+void set_launch_parts_wz(int p);
+void launch_scan_lists_wz(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev_lists);
+void launch_coarse_keys_wz(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist, float* out,
+                           hipStream_t s, bool ip, float* T3, const float* cb, int M, float* xn_buf);
+void launch_coarse_select_wz(const float* keys, int64_t nq, int nlist, int nprobe, float* out_dis, int64_t* out_list,
+                             hipStream_t s, bool ip, const ListPlan* plan, const int64_t* list_off, int lo, int hi,
+                             const float* x, const float* cent, int d);
+}  // namespace chivf
+static int wz_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = std::getenv("IVFPQ_WZ");
+    m = !e ? 0 : std::string(e) == "coarse" ? 1 : std::string(e) == "scan" ? 2 : std::string(e) == "merge" ? 3 : 0;
+  }
+  return m;
+}
+static void wz_scan_lists(const chivf::ScanArgs& a, const chivf::ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
+  const int m = wz_mode();
+  if (m == 2 || m == 3) {
+    chivf::set_launch_parts_wz(m == 2 ? 1 : 2);
+    chivf::set_launch_parts(m == 2 ? 2 : 1);
+    if (m == 2) {
+      chivf::launch_scan_lists_wz(a, pl, s, ev);
+      chivf::launch_scan_lists(a, pl, s, nullptr);
+    } else {
+      chivf::launch_scan_lists(a, pl, s, ev);
+      chivf::launch_scan_lists_wz(a, pl, s, nullptr);
+    }
+    chivf::set_launch_parts_wz(3);
+    chivf::set_launch_parts(3);
+  } else {
+    chivf::launch_scan_lists(a, pl, s, ev);
+  }
+}
+#define launch_scan_lists(...) wz_scan_lists(__VA_ARGS__)
+#define launch_coarse_keys(...) (wz_mode() == 1 ? launch_coarse_keys_wz(__VA_ARGS__) : launch_coarse_keys(__VA_ARGS__))
+#define launch_coarse_select(...) \
+  (wz_mode() == 1 ? launch_coarse_select_wz(__VA_ARGS__) : launch_coarse_select(__VA_ARGS__))
+#endif
 
 namespace {
 
@@ -202,6 +246,13 @@ constexpr bool kTiledCoarse = TILED_COARSE;
 #define INFLIGHT_MAXK 64  // experiments: -DINFLIGHT_MAXK=1024 lets every k overlap
 #endif
 constexpr int kInflightMaxK = INFLIGHT_MAXK;
+// Experiment (-DINFLIGHT_SCAN_ORDER=1): with batches in flight, overlap only a batch's
+// coarse step with the searches still in flight (its list scan waits for every other
+// stream's search).  Measured: still 2 wrong batches in 24000 at two streams, and slower
+// (profiles/r04_race.txt item 11), so off.
+#ifndef INFLIGHT_SCAN_ORDER
+#define INFLIGHT_SCAN_ORDER 0
+#endif
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
@@ -906,6 +957,7 @@ struct ivfpq_index {
                             d_off.as<int64_t>(), list_lo, list_hi, ip(), false, k, plan, s);
       }
       mark_end(tm, s);
+      if (INFLIGHT_SCAN_ORDER && inflight) order_after_all(s);  // the scans of different batches never overlap
       const float* T3 = W().w_T3.as<float>();
       if (preassigned && use_pre) {  // T3 computed ahead on another stream
         if (pre[pi].ready_stream != s) HIPCHECK(hipStreamWaitEvent(s, pre[pi].ready, 0));

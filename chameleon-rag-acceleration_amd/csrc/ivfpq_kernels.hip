@@ -4321,6 +4321,10 @@ int device_cus() {
   return cus;
 }
 
+#ifdef WZ_BISECT  // experiment: which launches of a search run from a forcezero build (profiles/build_wz_bisect.sh)
+int g_launch_parts = 3;  // bit 0: the list scan, bit 1: the merges
+void set_launch_parts(int p) { g_launch_parts = p; }
+#endif
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
@@ -4331,6 +4335,9 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
 #endif
   constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : JB_WIDE;
   if (ev) (void)hipEventRecord(ev[0], s);
+#ifdef WZ_BISECT
+  if (g_launch_parts & 1) {
+#endif
   if constexpr (G == 4 && R == 1 && M <= 16 && SCAN_PIPE) {
     if (a.k <= 16 && pl.fused) {  // one workgroup per CU
       hipLaunchKernelGGL((k_scan_pipe<M, 2>), dim3((unsigned)device_cus()), dim3(kPipeT), 0, s, a, pl);
@@ -4348,6 +4355,10 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   } else {
     hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   }
+#ifdef WZ_BISECT
+  }
+  if (!(g_launch_parts & 2)) return;
+#endif
   if (ev) (void)hipEventRecord(ev[1], s);
   if (R >= 2 && a.nprobe <= 64) {
     if (MERGE_RADIX && 4 * a.nprobe * pl.ks <= kRadixU * 256)  // every key of a query in one workgroup's registers
