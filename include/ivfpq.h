@@ -132,6 +132,7 @@ int ivfpq_search_preassigned_tables_device(ivfpq_index* h, int64_t n, const floa
 
 /* Batches in flight (see "Stream ordering" above): 1 = device searches on different
  * streams overlap, 0 = each waits for the others (default, unless IVFPQ_INFLIGHT=1).
+ * Experimental: ~1e-4 of overlapped batches differ from the oracle.
  * Waits for the handle's in-flight searches before switching.  Reference: the query
  * blocks streamed through one GPU index, bench_gpu_1bn.py:788-806. */
 int ivfpq_set_inflight(ivfpq_index* h, int on);
