@@ -94,7 +94,8 @@ def parse():
     p.add_argument("--inflight", type=int, default=1,
                    help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 turns the "
                         "index's batches-in-flight mode on so that consecutive batches overlap, DESIGN.md "
-                        "section 4 -- experimental: ~1e-4 of overlapped batches differ from the oracle); "
+                        "section 4 -- experimental, needs a -DIVFPQ_OVERLAP=1 build: ~1e-4 of overlapped batches "
+                        "differ from the oracle); "
                         "1 = one batch at a time on one stream (the parity-clean path, default)")
     return p.parse_args()
 
@@ -153,6 +154,9 @@ def main():
     xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
     k = args.k
     inflight = max(1, args.inflight)
+    if inflight > 1 and not faiss.overlap_built():
+        raise SystemExit("--inflight > 1 needs the experimental overlap, which this library was built without "
+                         "(-DIVFPQ_OVERLAP=1; DESIGN.md section 4)")
     ix.inflight = inflight > 1
     streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
     Dbufs = [torch.empty((Bg, k), dtype=torch.float32, device=dev) for _ in range(inflight)]
@@ -255,7 +259,7 @@ def main():
         for s in range(n_ex):
             ix.search(xq_host[s % args.nbatches], k)
         extra["host_search_queries_per_s"] = n_ex * Bg / (time.perf_counter() - t0)
-        if inflight == 1:  # the experimental overlap mode, two streams, reported beside the value only
+        if inflight == 1 and faiss.overlap_built():  # experimental overlap (-DIVFPQ_OVERLAP=1 builds), beside the value only
             st2 = [torch.cuda.Stream(dev) for _ in range(2)]
             D2 = [torch.empty_like(Dbuf) for _ in range(2)]
             I2 = [torch.empty_like(Ibuf) for _ in range(2)]
@@ -272,9 +276,9 @@ def main():
             finally:
                 ix.inflight = False
         extra["note"] = (f"{n_ex} batches each; k100 = search_device with k=100 (one stream: k > 64 searches "
-                         f"are not overlapped); overlap2 = {args.steps} steps with two batches in flight on two "
-                         f"streams (experimental, not the value: 2 in 24000 such batches differed from the "
-                         f"oracle, profiles/r04_race_rate.jsonl); "
+                         f"are not overlapped); overlap2 (only in a -DIVFPQ_OVERLAP=1 build) = {args.steps} steps with two "
+                         f"batches in flight on two streams (experimental, not the value: 2 in 24000 such batches "
+                         f"differed from the oracle, profiles/r04_race_rate.jsonl); "
                          f"host_search = search() on numpy "
                          f"queries (H2D copy, search, D2H copy; synchronous)")
     if world > 1:

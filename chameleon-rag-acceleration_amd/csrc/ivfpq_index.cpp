@@ -253,13 +253,19 @@ constexpr int kInflightMaxK = INFLIGHT_MAXK;
 #ifndef INFLIGHT_SCAN_ORDER
 #define INFLIGHT_SCAN_ORDER 0
 #endif
+// The overlap of batches in flight is experimental and not built by default: about 1
+// overlapped batch in 10^4 differs from the oracle (DESIGN.md section 4,
+// profiles/r04_race.txt).  -DIVFPQ_OVERLAP=1 builds it (profiles/build_variants.sh).
+#ifndef IVFPQ_OVERLAP
+#define IVFPQ_OVERLAP 0
+#endif
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
 // another stream.  IVFPQ_INFLIGHT=1 in the environment turns it on for new handles.
 bool inflight_default() {
   const char* e = std::getenv("IVFPQ_INFLIGHT");
-  return e && e[0] == '1';
+  return IVFPQ_OVERLAP && e && e[0] == '1';
 }
 
 }  // namespace
@@ -1442,12 +1448,17 @@ int ivfpq_set_inflight(ivfpq_index* h, int on) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     require(on == 0 || on == 1, "inflight must be 0 or 1");
+    require(on == 0 || IVFPQ_OVERLAP,
+            "batches-in-flight overlap is not built: it is experimental (about 1 overlapped batch in 10^4 differs "
+            "from the oracle, DESIGN.md section 4); build with -DIVFPQ_OVERLAP=1 to use it");
     h->quiesce();  // searches issued under the previous setting complete first
     h->inflight = on == 1;
   });
 }
 
 int ivfpq_get_inflight(const ivfpq_index* h) { return h ? (h->inflight ? 1 : 0) : -1; }
+
+int ivfpq_overlap_built(void) { return IVFPQ_OVERLAP ? 1 : 0; }
 
 int ivfpq_get_error_count(ivfpq_index* h, int64_t* out) {
   return guarded([&] {

@@ -19,6 +19,7 @@ from .index import (  # noqa: F401
     get_num_gpus,
     index_factory,
     merge_topk_device,
+    overlap_built,
     read_index,
     swig_ptr,
     vector_to_array,

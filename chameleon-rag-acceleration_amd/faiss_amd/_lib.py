@@ -39,6 +39,7 @@ SIGNATURES = {
                                                               ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]),
     "ivfpq_set_inflight": (ctypes.c_int, [c_handle, ctypes.c_int]),
     "ivfpq_get_inflight": (ctypes.c_int, [c_handle]),
+    "ivfpq_overlap_built": (ctypes.c_int, []),
     "ivfpq_get_error_count": (ctypes.c_int, [c_handle, c_i64p]),
     "ivfpq_add_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),

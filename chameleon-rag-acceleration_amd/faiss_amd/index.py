@@ -220,6 +220,12 @@ class _InvertedLists:
         return float(len(s) * (s * s).sum() / (tot * tot)) if tot else 0.0
 
 
+
+def overlap_built():
+    """True when the loaded library has the experimental batches-in-flight overlap
+    (ivfpq_overlap_built; built with -DIVFPQ_OVERLAP=1)."""
+    return bool(_lib.load().ivfpq_overlap_built())
+
 class IndexIVFPQ:
     """faiss.IndexIVFPQ (by_residual; METRIC_L2 with precomputed tables, or
     METRIC_INNER_PRODUCT) on one MI355X."""
@@ -488,7 +494,10 @@ class IndexIVFPQ:
         """Batches in flight: True lets device searches issued on different
         streams overlap (each stream keeps its own workspace, up to three);
         False (default, unless IVFPQ_INFLIGHT=1 at creation) orders each search
-        after those still in flight on other streams.  Results are the same."""
+        after those still in flight on other streams.  The overlap is
+        experimental and only in a library built with -DIVFPQ_OVERLAP=1
+        (``overlap_built()``): about 1 overlapped batch in 10^4 differs from the
+        oracle; setting True otherwise raises."""
         return bool(_lib.load().ivfpq_get_inflight(self._h))
 
     @inflight.setter

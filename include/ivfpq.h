@@ -132,11 +132,15 @@ int ivfpq_search_preassigned_tables_device(ivfpq_index* h, int64_t n, const floa
 
 /* Batches in flight (see "Stream ordering" above): 1 = device searches on different
  * streams overlap, 0 = each waits for the others (default, unless IVFPQ_INFLIGHT=1).
- * Experimental: ~1e-4 of overlapped batches differ from the oracle.
+ * Experimental, not built by default (ivfpq_overlap_built): ~1e-4 of overlapped
+ * batches differ from the oracle.
  * Waits for the handle's in-flight searches before switching.  Reference: the query
  * blocks streamed through one GPU index, bench_gpu_1bn.py:788-806. */
 int ivfpq_set_inflight(ivfpq_index* h, int on);
 int ivfpq_get_inflight(const ivfpq_index* h);
+/* 1 when the library was built with the overlap (-DIVFPQ_OVERLAP=1); otherwise
+ * ivfpq_set_inflight(h, 1) fails with a message and searches are always ordered. */
+int ivfpq_overlap_built(void);
 
 /* Index checks of the merge kernels: code positions read back from partial lists
  * outside the image, partial-list lengths above k and pair ids outside the batch

@@ -46,6 +46,10 @@ def rate(ix, xq_dev, k, reps):
     ms = e0.elapsed_time(e1) / reps
     # the same batches two in flight (batch r on stream r % 2, own outputs; wall clock
     # between device-wide synchronisations), as bench.py's timed region
+    import faiss_amd
+
+    if not faiss_amd.overlap_built():  # the experimental overlap is not in this build (-DIVFPQ_OVERLAP=1)
+        return {"k": k, "ms_per_batch": ms, "queries_per_s": B / (ms * 1e-3)}
     ss = [torch.cuda.Stream() for _ in range(2)]
     outs = [(D, I), (torch.empty_like(D), torch.empty_like(I))]
     ix.inflight = True

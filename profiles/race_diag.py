@@ -7,7 +7,8 @@ searched alone.  Per (k, streams, round): mismatching batches / rows, whether
 the bad rows hold sentinel labels or non-finite keys, and the merge kernels'
 index-check count.  Round 0 of each configuration is the first use of the
 workspaces at that k (buffers grow there); later rounds reuse them.
-Prints one JSON line per configuration."""
+Prints one JSON line per configuration.  The overlap cases need a library built with
+-DIVFPQ_OVERLAP=1 (profiles/build_variants.sh ov:"-DIVFPQ_OVERLAP=1", then IVFPQ_LIB=...)."""
 import json
 import os
 import sys

@@ -100,7 +100,7 @@ def main():
                 faiss.merge_topk_device(torch.stack([Dp[:B]] * N), torch.stack([Ip[:B]] * N))
 
         wall = {}
-        for label, depth in (("serial", 1), ("inflight2", 2)):
+        for label, depth in (("serial", 1), ("inflight2", 2))[:2 if faiss.overlap_built() else 1]:
             sh.inflight = depth > 1
             for s in range(4):
                 rank_step(s % depth)
