@@ -9,15 +9,15 @@ k=10, query batch 1024.  One *step* = one whole search of one 1024-query batch
 already resident in HBM.
 
 N > 1 (one process per GPU, torch.distributed over RCCL; weak scaling, 1024
-queries per GPU per step).  Default ``--mode replicas``: queries are independent
-units, and the C2 index (16 MB of codes) fits every GPU many times over, so each
-rank holds the whole index and searches its own batches -- no collective on the
-data path (the task's rule for partitionable units).  ``--mode shard`` is the
-path for an index that does not fit one GPU (C4: 1e9 vectors): the index is
-split by inverted-list range, each rank runs the coarse quantizer on its own
-1024-query slice, an all_gather shares the (list, dis0) probe arrays, every rank
-scans its lists for the whole batch (search_preassigned) and an all_to_all
+queries per GPU per step).  Default ``--mode shard``, the north_star design: the
+index is split by inverted-list range, each rank runs the coarse quantizer on its
+own 1024-query slice, an all_gather shares the (list, dis0) probe arrays, every
+rank scans its lists for the whole batch (search_preassigned) and an all_to_all
 returns each query slice's partials to its owner, which merges them on the GPU.
+Beside it (``extra.replicas``) the same ranks also time query-sharded replicas
+(each rank holds the whole index and searches its own batches, no collective on
+the data path) and check that the sharded results equal the replica's, bit for
+bit.  ``--mode replicas`` makes the replicas the value.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with
 ``roofline`` (the scan kernel's algorithmic code bytes / its HIP-event-timed
@@ -80,7 +80,7 @@ def parse():
     p.add_argument("--centres", type=int, default=200_000,
                    help="Gaussian centres of the synthetic generator (200k: the recall curve tracks SIFT1M's; "
                         "rounds 1-2 used 10k)")
-    p.add_argument("--mode", choices=["shard", "replicas"], default="replicas")
+    p.add_argument("--mode", choices=["shard", "replicas"], default="shard")
     p.add_argument("--cpu-sample", type=int, default=10240, help="queries in the CPU-baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (repetitions)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -286,6 +286,43 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    if shard:
+        # Beside the sharded value: query-sharded replicas (every rank the whole index,
+        # its own slice of each global batch) on the same ranks, and the sharded results
+        # checked against the replica's search of the same queries (bit for bit).
+        ix_rep = faiss.IndexIVFPQ(None, args.d, args.nlist, args.M, 8, device=local_rank)
+        ix_rep.set_trained(ix.centroids(), ix.codebook())
+        ix_rep.add(xb)
+        ix_rep.nprobe = args.nprobe
+        mine = [xq_dev[b][rank * B:(rank + 1) * B].contiguous() for b in range(args.nbatches)]
+        agree, rows = 0, 0
+        for b in range(args.nbatches):
+            step(b)
+            Dr, Ir = ix_rep.search_device(mine[b], k)
+            torch.cuda.synchronize()
+            Dm, Im = merged[b]
+            agree += int(((Im == Ir).all(dim=1) & (Dm == Dr).all(dim=1)).sum().item())
+            rows += B
+        for b in range(args.warmup):
+            ix_rep.search_device(mine[b % args.nbatches], k, Dbuf[:B], Ibuf[:B])
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            ix_rep.search_device(mine[s % args.nbatches], k, Dbuf[:B], Ibuf[:B])
+        torch.cuda.synchronize()
+        dist.barrier()
+        tr = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(tr, op=dist.ReduceOp.MAX)
+        ag = torch.tensor([agree, rows], dtype=torch.int64, device=dev)
+        dist.all_reduce(ag)
+        extra["replicas"] = {"queries_per_s": args.steps * B * world / float(tr.item()),
+                             "ms_per_step": float(tr.item()) * 1e3 / args.steps,
+                             "note": "each rank the whole index and its own 1024 queries per step, no collective"}
+        extra["shard_vs_replica_rows_identical"] = f"{int(ag[0].item())} / {int(ag[1].item())}"
+        del ix_rep
+
     queries = args.steps * B * world  # all ranks together
     qps = queries / elapsed
     ms_per_step = elapsed * 1000.0 / args.steps
@@ -356,29 +393,63 @@ def main():
             ox.ntotal = ix.ntotal
             ox.nprobe = args.nprobe
             ns = min(args.cpu_sample, nq_total)
-            # this process's share of the host: the cores in its affinity set, capped by
-            # OMP_NUM_THREADS (the GPU box's per-GPU CPU share is 16 and its pool asks
-            # worker pools to stay within it)
+            # This process's share of the host: the GPU pool gives each GPU's jobs 16 host
+            # cores and sets OMP_NUM_THREADS=16 on the box for it ("size worker pools to the
+            # box's CPU share (16 for one GPU)"; os.sched_getaffinity there lists the whole
+            # machine, which other GPUs' jobs share), so the oracle runs OMP_NUM_THREADS
+            # threads when set, else every core of the affinity set (e.g. this container).
             affinity = len(os.sched_getaffinity(0))
-            threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or affinity, affinity)
-            ox.search(xq[:64], k, threads)  # warm
-            rates, tc, Ic = [], 0.0, None
-            while len(rates) < 5 or (tc < args.cpu_seconds and len(rates) < 200):  # bounded: ~cpu_seconds
-                t0 = time.perf_counter()
-                Dc, Ic = ox.search(xq[:ns], k, threads)
-                dt = time.perf_counter() - t0
-                rates.append(ns / dt)
-                tc += dt
+            omp = os.environ.get("OMP_NUM_THREADS")
+            threads = min(int(omp or 0) or affinity, affinity)
+
+            def cpu_rate(nprobe_c):
+                ox.nprobe = nprobe_c
+                ox.search(xq[:64], k, threads)  # warm
+                rates, tc, Ic = [], 0.0, None
+                while len(rates) < 5 or (tc < args.cpu_seconds and len(rates) < 200):  # bounded: ~cpu_seconds
+                    t0 = time.perf_counter()
+                    _, Ic = ox.search(xq[:ns], k, threads)
+                    dt = time.perf_counter() - t0
+                    rates.append(ns / dt)
+                    tc += dt
+                return float(np.median(rates)), len(rates), tc, Ic
+
+            rate, nrep, tc, Ic = cpu_rate(args.nprobe)
             agree = None
             if not shard:
                 Ig = np.concatenate([ix.search(xq[i0:i0 + B], k)[1] for i0 in range(0, ns, B)])
                 agree = float((Ig == Ic).mean())
-            cpu_baseline = {"value": float(np.median(rates)), "unit": "queries/s", "cores": threads, "kind": "port",
+            cpu_baseline = {"value": rate, "unit": "queries/s", "cores": threads, "kind": "port",
                             "cpu_model": cpu_model(), "cores_in_affinity": affinity,
+                            "omp_num_threads_env": omp,
+                            "cores_note": "the GPU pool's per-GPU host share is 16 cores, exported as "
+                                          "OMP_NUM_THREADS=16 on the box (its rule: size worker pools to that "
+                                          "share); without OMP_NUM_THREADS every core of the affinity set runs",
                             "sample": f"{ns} of the same queries (batch {B}), k={k}, nprobe={args.nprobe}, same "
                                       f"trained index; oracle/ivfpq_oracle.c (Faiss-1.7.1 order, scalar C, "
-                                      f"OpenMP over queries); median of {len(rates)} repetitions, {tc:.1f}s total",
+                                      f"OpenMP over queries); median of {nrep} repetitions, {tc:.1f}s total",
                             "gpu_id_agreement": agree}
+            # BASELINE.json configs[0] (C1): the same index searched on the CPU at nprobe 8
+            # (the reference publishes 0.164 ms/query and R1@10 0.8317 on SIFT1M,
+            # Faiss_experiments/README.md:271), beside the GPU rate at nprobe 8
+            rate8, nrep8, tc8, I8 = cpu_rate(8)
+            c1 = {"cpu_queries_per_s": rate8, "cpu_ms_per_query_per_core": threads * 1e3 / rate8,
+                  "cores": threads, "repetitions": nrep8, "seconds": round(tc8, 1),
+                  "reference_sift1m": {"ms_per_query": 0.164, "R1@10": 0.8317}}
+            if not shard:
+                ix.nprobe = 8
+                xd8 = xq_dev[0]
+                ix.search_device(xd8, k, Dbuf, Ibuf)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for s in range(args.steps):
+                    ix.search_device(xq_dev[s % args.nbatches], k, Dbuf, Ibuf)
+                torch.cuda.synchronize()
+                c1["gpu_queries_per_s"] = args.steps * B / (time.perf_counter() - t0)
+                ix.nprobe = args.nprobe
+                if recall is not None:
+                    c1["R1@10_cpu_sample"] = datasets.recall_1_at(I8, gt[:ns], (1, k)).get(k)
+            cpu_baseline["c1_nprobe8"] = c1
 
     traffic = None
     traffic_src = "no counter file"

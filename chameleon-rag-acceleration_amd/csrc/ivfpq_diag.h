@@ -5,7 +5,7 @@
 // every macro below is empty.
 #pragma once
 
-#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS) || defined(DIAG_PSTAMPS)
+#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS)
 namespace chivf {
 constexpr int kDiagWG = 1024, kDiagItems = 64, kDiagSlots = 16;
 __device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
@@ -46,20 +46,4 @@ __device__ uint64_t g_diag[kDiagWG * kDiagItems * kDiagSlots];
   do {                \
   } while (0)
 #define DIAG_ONLY(...)
-#endif
-
-#ifdef DIAG_PSTAMPS  // pipelined scan: per (workgroup, phase) stamps of lane 0 of the stamping wave
-#define PDIAG(slot, v)                                                                     \
-  do {                                                                                     \
-    if (lane == 0 && blockIdx.x < kDiagWG && P < kDiagItems)                               \
-      g_diag[((size_t)blockIdx.x * kDiagItems + P) * kDiagSlots + (slot)] = (uint64_t)(v); \
-  } while (0)
-#define PDIAG_WAIT() __builtin_amdgcn_s_waitcnt(0)
-#else
-#define PDIAG_WAIT() \
-  do {               \
-  } while (0)
-#define PDIAG(slot, v) \
-  do {                 \
-  } while (0)
 #endif

@@ -29,50 +29,6 @@
 #include "ivfpq_build.h"
 
 using namespace chivf;
-#ifdef WZ_BISECT
-// experiment (profiles/build_wz_bisect.sh): the launchers of a forcezero build of the
-// kernels, chosen per search stage by IVFPQ_WZ = coarse | scan | merge
-namespace chivf {
-void set_launch_parts(int p);
-void set_launch_parts_wz(int p);
-void launch_scan_lists_wz(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev_lists);
-void launch_coarse_keys_wz(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist, float* out,
-                           hipStream_t s, bool ip, float* T3, const float* cb, int M, float* xn_buf);
-void launch_coarse_select_wz(const float* keys, int64_t nq, int nlist, int nprobe, float* out_dis, int64_t* out_list,
-                             hipStream_t s, bool ip, const ListPlan* plan, const int64_t* list_off, int lo, int hi,
-                             const float* x, const float* cent, int d);
-}  // namespace chivf
-static int wz_mode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = std::getenv("IVFPQ_WZ");
-    m = !e ? 0 : std::string(e) == "coarse" ? 1 : std::string(e) == "scan" ? 2 : std::string(e) == "merge" ? 3 : 0;
-  }
-  return m;
-}
-static void wz_scan_lists(const chivf::ScanArgs& a, const chivf::ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
-  const int m = wz_mode();
-  if (m == 2 || m == 3) {
-    chivf::set_launch_parts_wz(m == 2 ? 1 : 2);
-    chivf::set_launch_parts(m == 2 ? 2 : 1);
-    if (m == 2) {
-      chivf::launch_scan_lists_wz(a, pl, s, ev);
-      chivf::launch_scan_lists(a, pl, s, nullptr);
-    } else {
-      chivf::launch_scan_lists(a, pl, s, ev);
-      chivf::launch_scan_lists_wz(a, pl, s, nullptr);
-    }
-    chivf::set_launch_parts_wz(3);
-    chivf::set_launch_parts(3);
-  } else {
-    chivf::launch_scan_lists(a, pl, s, ev);
-  }
-}
-#define launch_scan_lists(...) wz_scan_lists(__VA_ARGS__)
-#define launch_coarse_keys(...) (wz_mode() == 1 ? launch_coarse_keys_wz(__VA_ARGS__) : launch_coarse_keys(__VA_ARGS__))
-#define launch_coarse_select(...) \
-  (wz_mode() == 1 ? launch_coarse_select_wz(__VA_ARGS__) : launch_coarse_select(__VA_ARGS__))
-#endif
 
 namespace {
 
@@ -88,11 +44,6 @@ void require(bool ok, const std::string& msg) {
   if (!ok) throw std::runtime_error(msg);
 }
 
-#ifdef DEVBUF_GUARD
-// experiment: every buffer is followed by kGuard bytes of 0xA5; check_guard() reports
-// whether any of them changed (an out-of-bounds write past the buffer's end)
-constexpr size_t kGuard = 1 << 16;
-#endif
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -100,27 +51,9 @@ struct DevBuf {
     if (b <= bytes && p) return;
     release();
     if (b == 0) b = 16;
-#ifdef DEVBUF_GUARD
-    b = (b + 255) & ~(size_t)255;
-    HIPCHECK(hipMalloc(&p, b + kGuard));
-    HIPCHECK(hipMemset(static_cast<char*>(p) + b, 0xA5, kGuard));
-    HIPCHECK(hipDeviceSynchronize());
-    bytes = b;
-    return;
-#endif
     HIPCHECK(hipMalloc(&p, b));
     bytes = b;
   }
-#ifdef DEVBUF_GUARD
-  bool check_guard() const {
-    if (!p) return true;
-    std::vector<unsigned char> g(kGuard);
-    HIPCHECK(hipMemcpy(g.data(), static_cast<const char*>(p) + bytes, kGuard, hipMemcpyDeviceToHost));
-    for (unsigned char c : g)
-      if (c != 0xA5) return false;
-    return true;
-  }
-#endif
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -225,47 +158,13 @@ constexpr size_t kPartialBytes = size_t(2048) << 20;  // bound for a chunk's per
 // C2, nlist 1024: segmented 22.5 + 8.5 us + a separate T3 launch 13.0 us vs key
 // matrix 17.8 + 10.0 us with T3 in the same launch)
 constexpr int kSegmentedNlist = 8192;
-// nlist <= 1024: one fused coarse launch (keys in LDS) with -DFUSED_COARSE=1 -- an A/B
-// variant only: at C2 it takes 54 us per batch against 30 us for the key matrix +
-// k_coarse_select (64 workgroups of 16 queries cannot fill the chip; profiles/r04_ab.txt)
-#ifndef FUSED_COARSE
-#define FUSED_COARSE 0
-#endif
-constexpr bool kFusedCoarse = FUSED_COARSE;
-// large d (C3): 64-query x 128-centroid key tiles; -DTILED_COARSE=0 builds the A/B variant
-#ifndef TILED_COARSE
-#define TILED_COARSE 1
-#endif
-constexpr bool kTiledCoarse = TILED_COARSE;
-// Batches in flight overlap only searches with k <= 64 (the row-packed and one-row
-// top-k paths).  k > 64 searches (partial-list lengths, k_merge_radix / k_merge_big)
-// returned wrong rows in about 1 batch of 40 when two of them overlapped, and the
-// cause is not found (profiles/r04_race.txt): they are ordered after
-// every search in flight, in either mode.
-#ifndef INFLIGHT_MAXK
-#define INFLIGHT_MAXK 64  // experiments: -DINFLIGHT_MAXK=1024 lets every k overlap
-#endif
-constexpr int kInflightMaxK = INFLIGHT_MAXK;
-// Experiment (-DINFLIGHT_SCAN_ORDER=1): with batches in flight, overlap only a batch's
-// coarse step with the searches still in flight (its list scan waits for every other
-// stream's search).  Measured: still 2 wrong batches in 24000 at two streams, and slower
-// (profiles/r04_race.txt item 11), so off.
-#ifndef INFLIGHT_SCAN_ORDER
-#define INFLIGHT_SCAN_ORDER 0
-#endif
-// The overlap of batches in flight is experimental and not built by default: about 1
-// overlapped batch in 10^4 differs from the oracle (DESIGN.md section 4,
-// profiles/r04_race.txt).  -DIVFPQ_OVERLAP=1 builds it (profiles/build_variants.sh).
-#ifndef IVFPQ_OVERLAP
-#define IVFPQ_OVERLAP 0
-#endif
 // Default of a handle's batches-in-flight switch (ivfpq_set_inflight): with it
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
 // another stream.  IVFPQ_INFLIGHT=1 in the environment turns it on for new handles.
 bool inflight_default() {
   const char* e = std::getenv("IVFPQ_INFLIGHT");
-  return IVFPQ_OVERLAP && e && e[0] == '1';
+  return e && e[0] == '1';
 }
 
 }  // namespace
@@ -319,10 +218,7 @@ struct ivfpq_index {
   struct Work {
     DevBuf w_dist, w_lists, w_dis0, w_T3, w_cand;  // w_cand: large-nlist coarse segment candidates
     DevBuf w_qn;  // |x|^2 of the batch's queries (tiled coarse keys)
-    DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_D, p_I, p_N, p_done, p_tau, p_qmask;
-#ifdef PART_CHECK
-    DevBuf p_chk;  // experiment: per partial list (count, hash) as the scan wrote it
-#endif
+    DevBuf p_cnt, p_bucket, p_recs, p_hdr, p_part, p_N, p_pd0, p_done, p_tau, p_qmask, p_evlog;
     uint32_t epoch = 0;  // tag of the last batch planned in this workspace (ListPlan::tauq)
     // every use records `done` on its stream; the slot's next user (on another
     // stream) waits for it, and whatever frees or rewrites shared device buffers
@@ -337,15 +233,16 @@ struct ivfpq_index {
   int slot = 0;  // the workspace of the current (last begun) device call
   uint64_t uses = 0;
   bool inflight = inflight_default();
+  int fault_inj = 0;  // test hook (ivfpq_set_fault_injection): ListPlan::fault
   std::mutex mu;
 
   Work& W() { return work[slot]; }
   // The workspace of a device call on stream s: the one last used on s (stream
   // order already protects it, and a one-stream caller keeps a single
   // workspace), else the least recently used one, ordered after its last user.
-  // overlap: this call may run concurrently with calls on other streams (inflight mode
-  // and k <= kInflightMaxK); otherwise it is ordered after every call in flight
-  void begin_slot(hipStream_t s, bool overlap = true) {
+  // With inflight on, this call may run concurrently with calls on other streams;
+  // otherwise it is ordered after every call in flight.
+  void begin_slot(hipStream_t s) {
     int pick = -1;
     for (int i = 0; i < kSlots && pick < 0; i++)
       if (work[i].done_pending && work[i].done_stream == s) pick = i;
@@ -366,7 +263,7 @@ struct ivfpq_index {
       HIPCHECK(hipEventSynchronize(w.done));
       w.done_pending = false;
     }
-    if (!inflight || !overlap) order_after_all(s);
+    if (!inflight) order_after_all(s);
   }
   // ordered after every device call still in flight (for paths that touch the
   // shared staging buffers or T3-ahead state)
@@ -407,9 +304,13 @@ struct ivfpq_index {
       HIPCHECK(hipMemsetAsync(w.p_hdr.p, 0, w.p_hdr.bytes, s));
     }
     pl.ks = part_stride(k);
-    w.p_D.ensure(sizeof(float) * nq * np * 4 * pl.ks);
-    w.p_I.ensure(sizeof(int64_t) * nq * np * 4 * pl.ks);
-    w.p_N.ensure(sizeof(int32_t) * nq * np * 4);
+    w.p_part.ensure(sizeof(uint4) * nq * np * 4 * pl.ks);
+    w.p_N.ensure(sizeof(uint2) * nq * np * 4);
+    w.p_pd0.ensure(sizeof(float) * nq * np);
+    if (!w.p_evlog.p) {
+      w.p_evlog.ensure(sizeof(uint32_t) * 8 * kEvLog);
+      HIPCHECK(hipMemsetAsync(w.p_evlog.p, 0, w.p_evlog.bytes, s));
+    }
     if (!w.p_done.p || w.p_done.bytes < sizeof(int32_t) * nq) {  // kept zero between batches by k_merge_probes
       w.p_done.ensure(sizeof(int32_t) * nq);
       HIPCHECK(hipMemsetAsync(w.p_done.p, 0, w.p_done.bytes, s));
@@ -423,26 +324,22 @@ struct ivfpq_index {
       HIPCHECK(hipMemsetAsync(w.p_tau.p, 0xff, w.p_tau.bytes, s));
       w.epoch = 1;
     }
-    w.p_qmask.ensure(sizeof(uint64_t) * nq);
+    pl.qmw = (np + 63) / 64;
+    w.p_qmask.ensure(sizeof(uint64_t) * nq * pl.qmw);
     pl.cnt = w.p_cnt.as<int32_t>();
     pl.bucket = w.p_bucket.as<int2>();
     pl.recs = w.p_recs.as<int32_t>();
     pl.hdr = w.p_hdr.as<int32_t>();
-    pl.partD = w.p_D.as<float>();
-    pl.partI = w.p_I.as<int64_t>();
-    pl.partN = w.p_N.as<int32_t>();
+    pl.part = w.p_part.as<uint4>();
+    pl.partN = w.p_N.as<uint2>();
+    pl.pd0 = w.p_pd0.as<float>();
+    pl.evlog = w.p_evlog.as<uint32_t>();
+    pl.fault = fault_inj;
     pl.qdone = w.p_done.as<int32_t>();
     pl.tauq = w.p_tau.as<uint64_t>();
     pl.epoch = w.epoch;
     pl.err = w.p_hdr.as<int32_t>() + 15;
     pl.qmask = w.p_qmask.as<uint64_t>();
-#ifdef PART_CHECK
-    if (!w.p_chk.p || w.p_chk.bytes < sizeof(uint32_t) * 4 * nq * np * 4) {
-      w.p_chk.ensure(sizeof(uint32_t) * 4 * nq * np * 4);
-      HIPCHECK(hipMemsetAsync(w.p_chk.p, 0, w.p_chk.bytes, s));
-    }
-    pl.chk = w.p_chk.as<uint32_t>();
-#endif
     pl.order = d_order.p ? d_order.as<int32_t>() : nullptr;
     pl.fused = scan_fused_plan(nloc, pl.max_items, M) ? 1 : 0;
     return pl;
@@ -887,22 +784,15 @@ struct ivfpq_index {
                      const ListPlan* plan = nullptr, float* T3out = nullptr) {
     if (nlist >= kSegmentedNlist && np <= 64) {  // large nlist: no [c][nlist] key matrix
       W().w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist, d) * np);
-      W().w_qn.ensure(sizeof(float) * c);
       if (T3out) launch_ip_table(x, c, d, d_cb.as<float>(), M, ksub, T3out, s);
       launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, W().w_cand.as<uint64_t>(),
-                              dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>(),
-                              W().w_qn.as<float>());
-      return plan != nullptr;
-    }
-    if (kFusedCoarse && coarse_fused_ok(nlist, d, np)) {  // keys in LDS, selection in the same launch
-      launch_coarse_fused(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, dis, lists, s, ip(), plan,
-                          d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>(), T3out, d_cb.as<float>(), M);
+                              dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
       return plan != nullptr;
     }
     W().w_dist.ensure(sizeof(float) * c * nlist);
     W().w_qn.ensure(sizeof(float) * c);
     launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, W().w_dist.as<float>(), s, ip(), T3out,
-                       d_cb.as<float>(), M, kTiledCoarse ? W().w_qn.as<float>() : nullptr);
+                       d_cb.as<float>(), M, W().w_qn.as<float>());
     if (np <= 64) {
       launch_coarse_select(W().w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
                            list_hi, x, d_cent.as<float>(), d);
@@ -919,7 +809,7 @@ struct ivfpq_index {
     check_search(n, k);
     upload_lists();
     if (n == 0) return;
-    begin_slot(s, k <= kInflightMaxK);
+    begin_slot(s);
     const int np = preassigned ? nprobe : eff_nprobe();
     const int64_t qc = query_chunk(n, np, k);
     W().w_T3.ensure(sizeof(float) * qc * M * ksub);
@@ -963,7 +853,6 @@ struct ivfpq_index {
                             d_off.as<int64_t>(), list_lo, list_hi, ip(), false, k, plan, s);
       }
       mark_end(tm, s);
-      if (INFLIGHT_SCAN_ORDER && inflight) order_after_all(s);  // the scans of different batches never overlap
       const float* T3 = W().w_T3.as<float>();
       if (preassigned && use_pre) {  // T3 computed ahead on another stream
         if (pre[pi].ready_stream != s) HIPCHECK(hipStreamWaitEvent(s, pre[pi].ready, 0));
@@ -1007,14 +896,14 @@ struct ivfpq_index {
   }
 
   // The query chunk of a search: [c][nlist] keys, T3 and buckets within
-  // kChunkBytes; the per-wave partial lists ([c][np][4][k] keys + positions, 48 B
-  // per entry and query) within kPartialBytes, so large k still runs whole
-  // 1024-query batches (C3, k = 1000, nprobe 32: 1.5 MB per query).
+  // kChunkBytes; the per-wave partial lists ([c][np][4][k] 16-B records, 64 B per
+  // entry and query) within kPartialBytes, so large k still runs whole
+  // 1024-query batches (C3, k = 1000, nprobe 32: 2 MB per query).
   int64_t query_chunk(int64_t n, int np, int k) const {
     const int nloc = std::max(list_hi - list_lo, 1);
     const size_t per_q = std::max({(size_t)nlist * 4, (size_t)M * ksub * 4, (size_t)nloc * 16});
     return std::max<int64_t>(
-        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * part_stride(k) * 48))}));
+        1, std::min<int64_t>({n, (int64_t)(kChunkBytes / per_q), (int64_t)(kPartialBytes / ((size_t)np * part_stride(k) * 64))}));
   }
 
   // T3 [n][M][ksub] of the queries x, on stream s, ahead of a preassigned search
@@ -1448,9 +1337,6 @@ int ivfpq_set_inflight(ivfpq_index* h, int on) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     require(on == 0 || on == 1, "inflight must be 0 or 1");
-    require(on == 0 || IVFPQ_OVERLAP,
-            "batches-in-flight overlap is not built: it is experimental (about 1 overlapped batch in 10^4 differs "
-            "from the oracle, DESIGN.md section 4); build with -DIVFPQ_OVERLAP=1 to use it");
     h->quiesce();  // searches issued under the previous setting complete first
     h->inflight = on == 1;
   });
@@ -1458,7 +1344,7 @@ int ivfpq_set_inflight(ivfpq_index* h, int on) {
 
 int ivfpq_get_inflight(const ivfpq_index* h) { return h ? (h->inflight ? 1 : 0) : -1; }
 
-int ivfpq_overlap_built(void) { return IVFPQ_OVERLAP ? 1 : 0; }
+int ivfpq_overlap_built(void) { return 1; }
 
 int ivfpq_get_error_count(ivfpq_index* h, int64_t* out) {
   return guarded([&] {
@@ -1474,30 +1360,57 @@ int ivfpq_get_error_count(ivfpq_index* h, int64_t* out) {
       HIPCHECK(hipMemcpy(hdr, w.p_hdr.p, sizeof(hdr), hipMemcpyDeviceToHost));
       tot += hdr[15];
     }
-#ifdef DEVBUF_GUARD
-    {
-#define GCHK(buf, name)                                               \
-  if (!(buf).check_guard()) {                                         \
-    std::fprintf(stderr, "[guard] overwritten past %s\n", name);     \
-    tot += 1000000000;                                                \
-  }
-      GCHK(h->d_cent, "d_cent") GCHK(h->d_centT, "d_centT") GCHK(h->d_cnorm, "d_cnorm") GCHK(h->d_cb, "d_cb")
-      GCHK(h->d_T1, "d_T1") GCHK(h->d_codes, "d_codes") GCHK(h->d_ids, "d_ids") GCHK(h->d_off, "d_off")
-      GCHK(h->d_order, "d_order") GCHK(h->w_x, "w_x") GCHK(h->w_xn, "w_xn") GCHK(h->w_D, "w_D") GCHK(h->w_I, "w_I")
-      GCHK(h->w_lno, "w_lno") GCHK(h->w_codes, "w_codes") GCHK(h->w_cent, "w_cent") GCHK(h->w_cn, "w_cn")
-      GCHK(h->h_D, "h_D") GCHK(h->h_I, "h_I") GCHK(h->h_Iq, "h_Iq") GCHK(h->h_Dq, "h_Dq")
-      GCHK(h->q_lists, "q_lists") GCHK(h->q_ids, "q_ids") GCHK(h->q_codes, "q_codes") GCHK(h->a_off, "a_off")
-      for (auto& pt : h->pre) GCHK(pt.buf, "pre.buf")
-      for (auto& w : h->work) {
-        GCHK(w.w_dist, "w_dist") GCHK(w.w_lists, "w_lists") GCHK(w.w_dis0, "w_dis0") GCHK(w.w_T3, "w_T3")
-        GCHK(w.w_cand, "w_cand") GCHK(w.w_qn, "w_qn") GCHK(w.p_cnt, "p_cnt") GCHK(w.p_bucket, "p_bucket")
-        GCHK(w.p_recs, "p_recs") GCHK(w.p_hdr, "p_hdr") GCHK(w.p_D, "p_D") GCHK(w.p_I, "p_I") GCHK(w.p_N, "p_N")
-        GCHK(w.p_done, "p_done") GCHK(w.p_tau, "p_tau") GCHK(w.p_qmask, "p_qmask")
-      }
-#undef GCHK
-    }
-#endif
     *out = tot;
+  });
+}
+
+int ivfpq_get_repair_stats(ivfpq_index* h, int64_t* stale_reads, int64_t* repairs) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(stale_reads != nullptr && repairs != nullptr, "null output");
+    h->quiesce();
+    int64_t st = 0, rp = 0;
+    for (auto& w : h->work) {
+      if (!w.p_hdr.p) continue;
+      int32_t hdr[16];
+      HIPCHECK(hipMemcpy(hdr, w.p_hdr.p, sizeof(hdr), hipMemcpyDeviceToHost));
+      st += hdr[kHdrStale];
+      rp += hdr[kHdrRepair];
+    }
+    *stale_reads = st;
+    *repairs = rp;
+  });
+}
+
+int ivfpq_get_repair_log(ivfpq_index* h, uint32_t* out, int max_events, int* n_events) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(n_events != nullptr && (out != nullptr || max_events == 0) && max_events >= 0, "bad output arguments");
+    h->quiesce();
+    int got = 0;
+    for (auto& w : h->work) {
+      if (!w.p_hdr.p || !w.p_evlog.p) continue;
+      int32_t hdr[16];
+      HIPCHECK(hipMemcpy(hdr, w.p_hdr.p, sizeof(hdr), hipMemcpyDeviceToHost));
+      const int kept = std::min(hdr[kHdrLog], kEvLog);
+      std::vector<uint32_t> ev((size_t)8 * kEvLog);
+      HIPCHECK(hipMemcpy(ev.data(), w.p_evlog.p, ev.size() * 4, hipMemcpyDeviceToHost));
+      for (int e = 0; e < kept && got < max_events; e++, got++) std::memcpy(out + 8 * got, &ev[8 * e], 32);
+    }
+    *n_events = got;
+  });
+}
+
+int ivfpq_set_fault_injection(ivfpq_index* h, int every) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    require(every >= 0, "fault injection period must be >= 0");
+    h->fault_inj = every;
   });
 }
 

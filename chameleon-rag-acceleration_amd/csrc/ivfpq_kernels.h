@@ -51,26 +51,15 @@ void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, 
                           hipStream_t s, bool ip, const ListPlan* plan = nullptr, const int64_t* list_off = nullptr,
                           int lo = 0, int hi = 0, const float* x = nullptr, const float* cent = nullptr, int d = 0);
 
-// Fused coarse quantizer (nlist <= 1024, nprobe <= 64; coarse_fused_ok): per 16
-// queries the keys of every centroid in LDS and the selection + planning of
-// launch_coarse_select in the same launch, which also builds T3 when T3out is set.
-bool coarse_fused_ok(int nlist, int d, int nprobe);
-void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist, int nprobe,
-                         float* out_dis, int64_t* out_list, hipStream_t s, bool ip, const ListPlan* plan,
-                         const int64_t* list_off, int lo, int hi, const float* cent, float* T3out, const float* cb,
-                         int M);
-
 // Large-nlist coarse quantizer without the key matrix: per (16 queries,
 // centroid segment) the nprobe (<= 64) best (key, list) words on the matrix
 // cores (cand [nq][coarse_segments(nq, nlist)][nprobe]), then per query their
 // merge, output and (with plan) the batch planning of launch_coarse_select.
-// xn_buf (nullable, [nq] floats of scratch): with d % 4 == 0 and nq >= 64 the segments
-// are walked by 64-query tiles (k_coarse_segtop_tiled, |x|^2 from launch_row_norms).
 int coarse_segments(int64_t nq, int nlist, int d);
 void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                              int nprobe, uint64_t* cand, float* out_dis, int64_t* out_list, hipStream_t s, bool ip,
                              const ListPlan* plan = nullptr, const int64_t* list_off = nullptr, int lo = 0, int hi = 0,
-                             const float* cent = nullptr, float* xn_buf = nullptr);
+                             const float* cent = nullptr);
 
 // y[i][j] = sum_t x[i][t] * AT[t][j] (t-ordered fmaf chain) + b[j] (b nullable): OPQ / LinearTransform apply
 void launch_linear_transform(const float* x, int64_t n, int d_in, const float* AT, const float* b, int d_out, float* y,
@@ -95,13 +84,15 @@ void launch_pq_encode(const float* x, int64_t n, int d, const float* cent, const
 // one pair per query).  Work items are (list, up to G pairs of one kind); all
 // kind-0 items are scheduled before kind-1 items, so each query's running
 // k-th key (tau) is usually known when its other probes are scanned.
-// Stride of one per-wave partial list in partD / partI: k (-DPART_PAD=1, an A/B
-// variant of the batches-in-flight investigation: k > 64 rounded up to 32 entries so
-// that every list owns whole 128-B lines)
-#ifndef PART_PAD
-#define PART_PAD 0
-#endif
-inline int part_stride(int k) { return (PART_PAD && k > 64) ? (k + 31) & ~31 : k; }
+// Stride of one per-wave partial list in `part`: k records of 16 B.
+inline int part_stride(int k) { return k; }
+
+// ListPlan::hdr words owned by the merges (hdr[0..1]: item counts, hdr[2]: the list
+// scan's work counter, hdr[15]: the index-check error word)
+constexpr int kHdrLog = 12;     // stale-entry events offered to the event log
+constexpr int kHdrStale = 13;   // (query, merge launch) pairs that read a stale entry
+constexpr int kHdrRepair = 14;  // probes rescanned by k_merge_probes
+constexpr int kEvLog = 64;      // events kept in ListPlan::evlog (8 words each)
 
 struct ListPlan {
   int32_t* cnt;      // [2][nloc] pair counts per kind; zero between batches (k_scan_lists re-zeroes)
@@ -110,9 +101,12 @@ struct ListPlan {
   int32_t* recs;     // [max_items][16] work items: list, count, size, beg(2), pairs[4], dis0[4]
   int32_t* hdr;      // [16]: n_items, n_items of kind 0, the list scan's work counter, 0...
   int max_items;
-  float* partD;      // [nq][nprobe][4 waves][k]  per-wave sorted partial top-k (keys)
-  int64_t* partI;    // same shape: global code positions (-1 = none; k <= 64 pads every list to k)
-  int32_t* partN;    // [nq][nprobe][4] valid entries of each partial list (k > 64 writes only those)
+  // [nq][nprobe][4 waves][k] per-wave sorted partial top-k, one 16-B record per entry:
+  // {key bits, tag, global code position lo, hi} (position -1 = none; k <= 64 pads
+  // every list to k).  tag = part_tag(epoch, slot) | writer XCD << 28 (ivfpq_kernels.hip)
+  uint4* part;
+  uint2* partN;      // [nq][nprobe][4] (valid entries, tag) of each partial list (k > 64 writes only those)
+  float* pd0;        // [nq][nprobe] the dis0 each planned pair was scanned with (a merge's rescan)
   int32_t* qdone;    // [nq] k > 64: 1 = merged by k_merge_big (k_merge_probes resets it to 0)
   // [nq] running k-th key per query, tagged with the batch: (~epoch) << 32 |
   // order-preserving key bits, lowered by 64-bit atomicMin.  A newer batch's
@@ -121,13 +115,15 @@ struct ListPlan {
   // initialised to all-ones.  Read with agent-scope atomic loads.
   uint64_t* tauq;
   uint32_t epoch;    // this batch's tag (>= 1, strictly increasing per workspace)
-  int32_t* err;      // [1] index-check violations counted by the merge kernels (0 = none; never reset)
-  uint64_t* qmask;   // [nq] probes the scan covers (nprobe <= 64): bit p = pair (q, p) is scanned
+  int32_t* err;      // [1] index-check violations counted by the merge kernels (0 = none; never reset; = hdr + 15)
+  uint64_t* qmask;   // [nq][qmw] probes the scan covers: bit p of word p / 64 = pair (q, p) is scanned
+  int qmw = 1;       // 64-bit mask words per query (ceil(nprobe / 64))
+  uint32_t* evlog;   // [kEvLog][8] the first stale-entry events (k_merge_probes log_stale)
+  int fault = 0;     // test hook (ivfpq_set_fault_injection): > 0 = slots with slot % fault == 1 are not written
   int grid;          // persistent list-scan workgroups (multiple of 8)
   const int32_t* order = nullptr;  // [nloc] item order of the lists within a kind (nullable = list order)
   int fused = 0;     // 1: the list scan derives its items from cnt/bucket (no k_plan_items launch, recs unused)
   int ks = 0;        // partial-list stride in entries (part_stride(k))
-  uint32_t* chk = nullptr;  // -DPART_CHECK experiment only: [nq][nprobe][4] (count, hash) of each partial list
 };
 
 struct ScanArgs {

@@ -586,6 +586,7 @@ __device__ __forceinline__ void plan_pair(const ListPlan& pl, int nloc, int64_t 
   const int s = atomicAdd(&pl.cnt[kind * nloc + (int)(l - lo)], 1);
   // a list holds at most one pair per query and kind, so s < cap (deduplicated rows)
   if (s < pl.cap) pl.bucket[((int64_t)(l - lo) * 2 + kind) * pl.cap + s] = make_int2(pair, __float_as_int(dis0));
+  pl.pd0[pair] = dis0;  // the same dis0 for a merge that has to rescan the pair (repair_probe)
 }
 
 // The query bound tau_q of this batch (an order-preserving int; "no bound" =
@@ -601,6 +602,28 @@ __device__ __forceinline__ void tau_lower(const ListPlan& pl, int64_t q, int o) 
   const uint64_t w = ((uint64_t)(~pl.epoch) << 32) | ((uint32_t)o ^ 0x80000000u);
   atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);
 }
+// ---- self-identifying partial lists ("Tagged partial lists")
+// Every per-wave partial-list entry is one 16-B record {key bits, tag, code
+// position (int64)} written by one store; the tag's low 28 bits name the batch
+// (the workspace epoch) and the slot, its high 4 bits the XCD of the writer.  A
+// reader that finds another tag has read memory this batch's scan did not leave
+// there (a lost, late or misdirected store): the merges never use such an entry
+// and rescan that probe's list instead (k_merge_probes, repair_probe).
+constexpr uint32_t kTagMask = 0x0FFFFFFFu;
+__device__ __forceinline__ uint32_t part_tag(uint32_t epoch, int64_t slot) {
+  return (epoch * 0x9E3779B1u + (uint32_t)slot) & kTagMask;
+}
+// this wave's XCD (hwreg XCC_ID bits 3:0) in the tag's top nibble
+__device__ __forceinline__ uint32_t xcc_tag() {
+  return ((uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 15u) << 28;
+}
+__device__ __forceinline__ uint4 part_rec(float key, uint32_t tag, int64_t pos) {
+  return make_uint4(__float_as_uint(key), tag, (uint32_t)(uint64_t)pos, (uint32_t)((uint64_t)pos >> 32));
+}
+__device__ __forceinline__ bool tag_ok(uint32_t t, uint32_t expect) { return ((t ^ expect) & kTagMask) == 0; }
+__device__ __forceinline__ float rec_key(const uint4& r) { return __uint_as_float(r.x); }
+__device__ __forceinline__ int64_t rec_pos(const uint4& r) { return (int64_t)(((uint64_t)r.w << 32) | r.z); }
+
 // a code position read back from a partial list, checked against the image
 // (counted in pl.err and dropped when outside it: never dereferenced)
 __device__ __forceinline__ bool pos_ok(const ScanArgs& a, const ListPlan& pl, int64_t pos) {
@@ -924,9 +947,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
 // Faiss tree order as coarse_stage_queries).  Workgroups past the key tiles build
 // T3 as in k_coarse_gemm.
 constexpr int TQ = 64, TC = 128, TKC = 32;
-#ifndef TILED_SEGTOP
-#define TILED_SEGTOP 0  // -DTILED_SEGTOP=1: k_coarse_segtop_tiled (A/B: 512 vs 390 us per 1024 queries at C4, profiles/r04_ab.txt)
-#endif
 constexpr int TAS = TKC + 2;   // A row stride (floats): 2 mod 32 -> conflict-free MFMA A reads
 constexpr int TBS = TC + 16;   // B row stride: 16 mod 32 -> conflict-free B reads
 
@@ -1051,50 +1071,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm_tiled(const float* __restri
   }
 }
 
-// T3 on the matrix cores -- a tolerance-mode A/B build only (-DT3_MFMA via
-// profiles/build_variants.sh; never the shipped library).  T3[q][m][j] =
-// <x_q[m], C_mj> as one 16 x 16 v_mfma_f32_16x16x4_f32 tile per (16 queries,
-// 16 codewords), K = dsub: a sequential fma chain over the sub-vector instead
-// of Faiss's 8-wide tree, so the LUT (and the ids of near-ties) can differ from
-// the oracle's.  Workgroup = 16 queries x one sub-quantizer; wave w: codewords
-// 64 w .. 64 w + 63.  profiles/r03_t3_mfma.txt has the A/B.
-#ifdef T3_MFMA
-__global__ __launch_bounds__(256) void k_t3_mfma(const float* __restrict__ x, int64_t nq, int d,
-                                                 const float* __restrict__ cb, int M, float* __restrict__ out) {
-  __shared__ float xs[16 * 16];  // [t][16 queries], t < dsub padded to 4
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int dsub = d / M, dk = (dsub + 3) & ~3;
-  const int64_t q0 = (int64_t)(blockIdx.x / M) * 16;
-  const int m = blockIdx.x % M;
-  for (int e = tid; e < 16 * dk; e += 256) {
-    const int t = e / 16, i = e % 16;
-    xs[e] = (t < dsub && q0 + i < nq) ? x[(q0 + i) * d + m * dsub + t] : 0.f;
-  }
-  __syncthreads();
-  const int i16 = lane & 15, k4 = lane >> 4;
-  f4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < dk; k0 += 4) {
-    const int kk = k0 + k4;
-    const float av = xs[kk * 16 + i16];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int j = wave * 64 + t * 16 + i16;
-      const float bv = kk < dsub ? cb[((int64_t)m * 256 + j) * dsub + kk] : 0.f;
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 4; t++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int64_t q = q0 + k4 * 4 + r;
-      if (q < nq) out[q * (int64_t)M * 256 + m * 256 + wave * 64 + t * 16 + i16] = acc[t][r];
-    }
-}
-#endif  // T3_MFMA
-
 // Write a query's top-nprobe (run: packed (key, list), ascending across the
 // wave) and, with cp.on, plan its probes for the list-major scan.
 // -<x_q, c_{l(p)}> in Faiss tree order (tree<K_IP> over d) for the probes p < np of one
@@ -1158,7 +1134,7 @@ __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, i
     const bool use = lane < nprobe && l >= cp.lo && l < cp.hi && cp.list_off[l + 1] > cp.list_off[l];
     const uint64_t um = __ballot(use);
     const int fp = um ? (int)__builtin_ctzll(um) : 64;
-    if (lane == 0) cp.pl.qmask[q] = um;  // the probes the scan covers (read by the merge)
+    if (lane == 0) cp.pl.qmask[q * cp.pl.qmw] = um;  // the probes the scan covers (read by the merge)
     float d0 = rd;
     if (ip && um) d0 = wave_ip_dis0(x + q * d, cp.cent, use ? l : -1, d, nprobe, lane);  // (wave-uniform)
     if (use) plan_pair(cp.pl, cp.hi - cp.lo, l, cp.lo, lane == fp ? 0 : 1, (int)(q * nprobe + lane), d0);
@@ -1170,7 +1146,7 @@ __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, i
 // nprobe-th smallest of the 64 lane minima (those minima are nprobe distinct
 // keys, so every member of the block's top-nprobe is at or below it), sorted
 // once and merged into the running list.  With `cp.on`, the epilogue plans
-// the batch exactly as k_coarse_fused did (first usable probe, tau reset,
+// the batch (first usable probe, per-list pair counts, bucket entries with the
 // bucket entries with the scan's dis0).
 // The nprobe (<= 64) smallest (key, list) words of one query's key row (global
 // or LDS), ascending across the wave (packed, kKcNone = none); scratch: 64 words
@@ -1233,96 +1209,6 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
   SDIAG(3);
   coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
   SDIAG(5);
-}
-
-// Fused coarse quantizer for nlist <= kFusedCoarseLists (C2): workgroup = 16
-// queries x every centroid.  Its 4 waves compute the key tiles (the
-// coarse_key_tile MFMA arithmetic of k_coarse_gemm) for all nlist centroids
-// into LDS, then each wave selects and plans 4 of the queries from there
-// (coarse_select_row + coarse_emit, as k_coarse_select): the [B x nlist] key
-// matrix never goes through HBM and the selection needs no second launch.
-// Workgroups past the key blocks build T3 as in k_coarse_gemm.
-constexpr int kFusedCoarseLists = 1024;
-
-__global__ __launch_bounds__(256) void k_coarse_fused(const float* __restrict__ x, int64_t nq, int d,
-                                                      const float* __restrict__ centT, int ldc,
-                                                      const float* __restrict__ cn, int nlist, int ip, int nprobe,
-                                                      float* __restrict__ out_dis, int64_t* __restrict__ out_list,
-                                                      int nkb, CoarseT3 t3, CoarsePlan cp) {
-  extern __shared__ __attribute__((aligned(16))) float g_lds[];
-  __shared__ uint64_t scratch[4][64];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  if ((int)blockIdx.x >= nkb) {  // ---- T3 role (k_coarse_gemm's)
-    const int tb = blockIdx.x - nkb;
-    const int total = t3.M * 256;
-    const int dsub = d / t3.M;
-    const int64_t q0 = (int64_t)(tb / t3.M) * GQ;
-    const int m = tb % t3.M;
-    const int e = m * 256 + tid;
-    float* xs = g_lds;
-    for (int i = tid; i < GQ * dsub; i += 256) {
-      const int qq = i / dsub;
-      xs[i] = q0 + qq < nq ? x[(q0 + qq) * d + m * dsub + (i - qq * dsub)] : 0.f;
-    }
-    __syncthreads();
-    const int nqq = (int)min<int64_t>(GQ, nq - q0);
-    if (dsub == 8) {
-      const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
-      const float4 c0 = src[0], c1 = src[1];
-      const float w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-      for (int qq = 0; qq < GQ; qq++) {
-        const float4* xv = reinterpret_cast<const float4*>(xs + qq * 8);
-        const float4 x0 = xv[0], x1 = xv[1];
-        const float xq[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        const float v = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return w[t]; }, 8);
-        if (qq < nqq) t3.out[(q0 + qq) * total + e] = v;
-      }
-    } else {
-      const float* cwp = t3.cb + (int64_t)e * dsub;
-      for (int qq = 0; qq < nqq; qq++) {
-        const float* xq = xs + qq * dsub;
-        t3.out[(q0 + qq) * total + e] = tree<K_IP>([&](int t) { return xq[t]; }, [&](int t) { return cwp[t]; }, dsub);
-      }
-    }
-    return;
-  }
-  // ---- keys of 16 queries x all centroids into LDS, then the selection
-  const int64_t q0 = (int64_t)blockIdx.x * GQ;
-  const int dk = (d + 63) & ~63;
-  float* xs = g_lds;            // [dk][GQ]
-  float* xn = xs + dk * GQ;     // [GQ] + 128 scratch
-  float* keys = xn + GQ * 9;    // [GQ][nlist]
-  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
-  __syncthreads();  // xn
-  const int i16 = lane & 15, k4 = lane >> 4;
-  for (int cb = 0; cb < nlist; cb += GC) {
-    const int c0 = cb + wave * 32;
-    f4 acc[NTL];
-    coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
-#pragma unroll
-    for (int t = 0; t < NTL; t++) {
-      const int c = c0 + t * 16 + i16;
-      if (c >= nlist) continue;
-      const float cnv = ip ? 0.f : cn[c];
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int i = k4 * 4 + r;
-        keys[i * nlist + c] = coarse_key(acc[t][r], xn[i], cnv, ip);
-      }
-    }
-  }
-  __syncthreads();
-#pragma unroll 1
-  for (int r = 0; r < 4; r++) {
-    const int i = wave * 4 + r;
-    const int64_t q = q0 + i;
-    if (q >= nq) break;  // wave-uniform
-    const uint64_t run = coarse_select_row(keys + i * nlist, nlist, nprobe, scratch[wave], lane);
-    coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
-  }
 }
 
 // ------------------------------------------------------ linear pre-transform
@@ -1466,7 +1352,7 @@ __global__ __launch_bounds__(256) void k_pq_encode(const float* __restrict__ x, 
 // One wave per query: tau reset, first usable probe, per-list pair counts and
 // bucket entries (the fused coarse epilogue does the same for its batch).
 // dedup (caller-supplied rows): a list repeated in a query's row is scanned
-// once, at its first position; the later pairs are reported as empty partials.
+// once, at its first position (the later pairs are left out of the probe mask).
 __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ lists, const float* __restrict__ Dq,
                                                     const float* __restrict__ x, const float* __restrict__ cent,
                                                     int64_t nq, int d, int nprobe,
@@ -1490,20 +1376,12 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
         dup = dup || (j < lane && lj == l);
       }
       for (int j = 0; j < p0 && use && !dup; j++) dup = lists[q * nprobe + j] == l;
-      if (use && dup) {  // the merge reads every usable pair's partial slots: write them empty
-        use = false;
-        const int64_t o = (q * nprobe + p) * 4 * (int64_t)pl.ks;
-        for (int e = 0; e < 4 * pl.ks; e++) {
-          pl.partD[o + e] = FLT_MAX;
-          pl.partI[o + e] = -1;
-        }
-        for (int w = 0; w < 4; w++) pl.partN[(q * nprobe + p) * 4 + w] = 0;
-      }
+      use = use && !dup;  // (its bit stays clear in qmask: the merge skips the pair)
     }
     const uint64_t um = __ballot(use);
     const int fp = (!found && um) ? (int)__builtin_ctzll(um) : 64;
     found = found || um != 0;
-    if (p0 == 0 && lane == 0) pl.qmask[q] = um;  // (nprobe <= 64 only: the merge reads it then)
+    if (lane == 0) pl.qmask[q * pl.qmw + (p0 >> 6)] = um;  // the pairs the scan covers (read by the merges)
     float d0 = 0.f;
     if (ip && um) d0 = wave_ip_dis0(x + q * d, cent, use ? l : -1, d, min(64, nprobe - p0), lane);  // (uniform)
     if (use) {
@@ -1615,7 +1493,7 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_small(ListPlan pl, const 
     ex[1][nloc] = cb;
   }
   const int T0 = ca, N = ca + cb;
-  if (blockIdx.x == 0 && tid < 16) pl.hdr[tid] = tid == 0 ? N : tid == 1 ? T0 : 0;
+  if (blockIdx.x == 0 && tid < 2) pl.hdr[tid] = tid == 0 ? N : T0;  // (hdr[2..] belong to the scan and merges)
   __syncthreads();
   const int e = blockIdx.x * PLAN_T + tid;
   if (e >= N) return;
@@ -1663,7 +1541,7 @@ __global__ __launch_bounds__(PLAN_T) void k_plan_items_big(ListPlan pl, const in
     ex0[PLAN_T] = sa;
     ex1[PLAN_T] = sb;
   }
-  if (blockIdx.x == 0 && tid < 16) pl.hdr[tid] = tid == 0 ? T0 + T1 : tid == 1 ? T0 : 0;
+  if (blockIdx.x == 0 && tid < 2) pl.hdr[tid] = tid == 0 ? T0 + T1 : T0;
   __syncthreads();
   const int own0 = ex0[PLAN_T], own1 = ex1[PLAN_T];
   for (int e = tid; e < own0 + own1; e += PLAN_T) {
@@ -2001,94 +1879,28 @@ __device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& p
   return v;
 }
 
-// A wave's sorted partial list of one pair into slot `slot` = pair * 4 + wave:
-// k <= 64 pads the list to k entries ((FLT_MAX, -1)); k > 64 writes the valid
-// entries and their count only (k_merge_big reads partN).
-#ifdef PART_CHECK
-__device__ __forceinline__ uint32_t part_hash(uint32_t kb, uint32_t pos, int ix) {
-  uint32_t h = kb * 0x9E3779B1u ^ (pos + 0x7F4A7C15u) * 0x85EBCA77u ^ (uint32_t)ix * 0xC2B2AE3Du;
-  return h ^ (h >> 15);
-}
-#endif
+// A wave's sorted partial list of one pair into slot `slot` = pair * 4 + wave, as
+// tagged records (part_rec): k <= 64 pads the list to k entries ((FLT_MAX, -1));
+// k > 64 writes the valid entries and their count only ((n, tag) in partN).
+// fault (test hook, ivfpq_set_fault_injection): slots with slot % fault == 1 are
+// not written at all, as if the stores were lost -- the merges must detect them.
 template <int R>
 __device__ __forceinline__ void write_partial(const ListPlan& pl, const PackedTopK<R>& tk, int64_t slot, int k,
                                               int64_t beg, int lane) {
-#if defined(WAIT_AT) && WAIT_AT == 1  // experiment: every memory result waited for before the partial writes
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
-  const int64_t o = slot * pl.ks;
+  if (pl.fault > 0 && slot % pl.fault == 1) return;  // (uniform; 0 in every real search)
+  const uint32_t tag = part_tag(pl.epoch, slot) | xcc_tag();
+  uint4* o = pl.part + slot * pl.ks;
   int n = 0;
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const int ix = r * 64 + lane;
     const bool empty = tk.p[r] == kKcNone;
-    if (ix < k && (R == 1 || !empty)) {
-#ifdef PART_WT  // experiment: write-through (agent-scope) partial stores
-      __hip_atomic_store(pl.partD + o + ix, empty ? FLT_MAX : kc_key(tk.p[r]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(pl.partI + o + ix, empty ? (int64_t)-1 : beg + (int64_t)(uint32_t)tk.p[r], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-#else
-      pl.partD[o + ix] = empty ? FLT_MAX : kc_key(tk.p[r]);
-      pl.partI[o + ix] = empty ? -1 : beg + (int64_t)(uint32_t)tk.p[r];  // global code position
-#endif
-    }
+    if (ix < k && (R == 1 || !empty))
+      o[ix] = part_rec(empty ? FLT_MAX : kc_key(tk.p[r]), tag, empty ? -1 : beg + (int64_t)(uint32_t)tk.p[r]);
     if constexpr (R >= 2) n += __popcll(__builtin_amdgcn_ballot_w64(ix < k && !empty));
   }
   if constexpr (R >= 2)
-    if (lane == 0) {
-#ifdef PART_WT
-      __hip_atomic_store(pl.partN + slot, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-      pl.partN[slot] = n;
-#endif
-    }
-#if defined(WAIT_AT) && WAIT_AT == 2  // experiment: ... after them
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
-#ifdef PART_CHECK
-  if constexpr (R >= 2) {
-    uint32_t h = 0;
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int ix = r * 64 + lane;
-      if (ix < k && tk.p[r] != kKcNone)
-        h ^= part_hash(__float_as_uint(kc_key(tk.p[r])), (uint32_t)(beg + (int64_t)(uint32_t)tk.p[r]), ix);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) h ^= (uint32_t)__shfl_xor((int)h, off, 64);
-    if (lane == 0) {
-      pl.chk[4 * slot] = (uint32_t)n;
-      pl.chk[4 * slot + 1] = h;
-      atomicAdd(pl.chk + 4 * slot + 2, 1u);  // writes of this partial list in this batch
-    }
-    // read back what this wave just stored (L1 bypass): +100 when it differs already
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t hs = 0;
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int ix = r * 64 + lane;
-      if (ix < k && tk.p[r] != kKcNone) {
-        const uint32_t kb = __hip_atomic_load(reinterpret_cast<const uint32_t*>(pl.partD) + o + ix, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t pb = __hip_atomic_load(reinterpret_cast<const uint64_t*>(pl.partI) + o + ix, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-        hs ^= part_hash(kb, (uint32_t)pb, ix);
-      }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) hs ^= (uint32_t)__shfl_xor((int)hs, off, 64);
-    if (lane == 0 && hs != h) atomicAdd(pl.err, 100);
-    // the written entries must be exactly indices 0 .. n - 1: +10000 per list with a hole
-    bool hole = false;
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int ix = r * 64 + lane;
-      hole = hole || (ix < n && tk.p[r] == kKcNone);
-    }
-    if (__builtin_amdgcn_ballot_w64(hole) && lane == 0) atomicAdd(pl.err, 10000);
-  }
-#endif
+    if (lane == 0) pl.partN[slot] = make_uint2((uint32_t)n, tag);
 }
 
 // ROWK (k <= 16, G = 4, R = 1): the 4 pairs' running top-k share one 64-bit
@@ -2170,13 +1982,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     }
 #pragma unroll
     for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
-#ifdef PART_CHECK
-    // experiment: the bucket's pair must be a probe of this list (probe_list, written by
-    // the same coarse launch as the bucket); a mismatch adds 100000000
-    if (lane == 0)
-      for (int g = 0; g < G; g++)
-        if (g < it.cnt && a.probe_list[it.pair[g]] != (int64_t)it.l) atomicAdd(pl.err, 100000000);
-#endif
   };
 
   if (tid == 0) {
@@ -2370,9 +2175,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       }
 #pragma unroll
       for (int g = 0; g < G; g++) qn[g] = 0;
-#if defined(WAIT_AT) && WAIT_AT == 3  // experiment: ... at the end of every queue drain
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
       loose = false;
 #pragma unroll
       for (int g = 0; g < G; g++) {
@@ -2624,11 +2426,11 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       int pr = it.pair[0];
 #pragma unroll
       for (int g = 1; g < G; g++) pr = rg == g ? it.pair[g] : pr;
-      if (rg < it.cnt && re < k) {
-        const int64_t o = ((int64_t)pr * 4 + wave) * pl.ks + re;
+      const int64_t slot = (int64_t)pr * 4 + wave;
+      if (rg < it.cnt && re < k && !(pl.fault > 0 && slot % pl.fault == 1)) {  // (fault: test hook, write_partial)
         const bool empty = rk == kKcNone;
-        pl.partD[o] = empty ? FLT_MAX : kc_key(rk);
-        pl.partI[o] = empty ? -1 : it.beg + (int64_t)(uint32_t)rk;
+        pl.part[slot * pl.ks + re] =
+            part_rec(empty ? FLT_MAX : kc_key(rk), part_tag(pl.epoch, slot) | xcc_tag(), empty ? -1 : it.beg + (int64_t)(uint32_t)rk);
       }
     } else {
 #pragma unroll
@@ -2644,534 +2446,6 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     DIAG(3, __builtin_amdgcn_s_memtime());
     it_no++;
     cur = nxt;
-  }
-#ifdef SCAN_REL
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // A/B: coherence experiment
-#endif
-#ifdef ORDER_CANARY
-  // stream-order experiment: count this workgroup's exit once all its waves are done
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(pl.hdr + 13, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#endif
-}
-
-// ------------------------------------------ pipelined list scan (k <= 16)
-// k_scan_pipe: the list scan of k_scan_lists<M, 4, 1, JB, true> (C2: M = 16,
-// k = 10) restructured so that the LUT build leaves the critical path.  One
-// 768-thread workgroup per CU: 8 scan waves scan item i out of LUT buffer i & 1
-// while 4 loader waves load item i + 1's T1 row and 4 T3 rows (80 KB at M = 16)
-// and write its LUT into the other buffer; one workgroup barrier per item hands
-// the buffers over.  Loader wave 8 also takes the item after next from the work
-// counter and stages its record words in LDS (3 slots: item i scanned, i + 1
-// built, i + 2 fetched), so the scan waves can start item i + 1's code loads
-// before that barrier.  The 8 scan waves split an item's codes (chunk of 64
-// codes per wave, 512 per step); waves w and w + 4 merge their row-packed
-// top-k in LDS at the next item's start and wave w writes the partial list of
-// slot (pair, w), so the merge kernels see the 4 per-wave lists per pair that
-// k_scan_lists writes.  Every candidate key is computed, admitted, queued and
-// ranked exactly as in k_scan_lists (same fp32 order, same (key, position)
-// ranking): results are identical.
-constexpr int kPipeScan = 8, kPipeLoad = 4, kPipeT = 64 * (kPipeScan + kPipeLoad);
-// candidate queue entries per scan wave: >= 64 per pair, so that a drained queue
-// always takes a whole 64-code chunk (the admission loop's progress guarantee)
-constexpr int kPipeQ = 256;
-
-template <int M, int JB>
-__global__ __launch_bounds__(kPipeT, 1) void k_scan_pipe(ScanArgs a, ListPlan pl) {
-  constexpr int G = 4;
-  constexpr int LUTN = M * 256;
-  constexpr int NV = LUTN / 4 / 256;  // float4 rows per loader thread and table
-  constexpr int QG = kPipeQ / G;
-  static_assert(QG >= 64, "a chunk's candidates must fit an empty queue");
-  constexpr int CH = 64 * kPipeScan;  // codes per chunk step of the workgroup
-  static_assert(JB % 2 == 0, "chunks are gathered in pairs");
-  __shared__ __attribute__((aligned(16))) float4 lut[2][LUTN];
-  __shared__ float qd[kPipeScan][kPipeQ];
-  __shared__ int32_t qi[kPipeScan][kPipeQ];
-  __shared__ uint16_t s_ex[2][kFusedPlanLists + 1];
-  __shared__ uint16_t s_ord[kFusedPlanLists];
-  __shared__ uint64_t s_rows[2][4][64];  // waves 4..7's top-k rows, merged by waves 0..3
-  __shared__ int32_t s_rec[3][16];       // record words of the items in flight (item mod 3)
-  __shared__ int32_t s_idx[3];           // their item numbers (-1: none)
-  __shared__ int32_t s_tq[2][G];         // the built item's query bounds (read by the loaders)
-  __shared__ int32_t s_wb[2][G];         // the item's bounds found by its scan waves
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int k = a.k;
-  const int ip = a.ip;
-  const int nloc = a.list_hi - a.list_lo;
-  const uint64_t lanemask_lt = (1ull << lane) - 1;
-  const float inv_np = 1.0f / (float)a.nprobe;
-  const int2 nn = fused_plan_prefix(pl, nloc, G, s_ex[0], s_ex[1], s_ord, reinterpret_cast<int*>(qi));
-  const int n_items0 = nn.x, n_items = nn.x + nn.y;
-
-  auto unpack = [&](Item<G>& it, int rv) __attribute__((always_inline)) {
-    it.l = __builtin_amdgcn_readlane(rv, 0);
-    const int t = __builtin_amdgcn_readlane(rv, 14);
-    it.cnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - t * G);
-    it.n = __builtin_amdgcn_readlane(rv, 2) - __builtin_amdgcn_readlane(rv, 3);
-    it.beg = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane(rv, 3));
-    it.kind = __builtin_amdgcn_readlane(rv, 13);
-#pragma unroll
-    for (int g = 0; g < G; g++) {
-      it.pair[g] = __builtin_amdgcn_readlane(rv, 5 + g);
-      it.d0[g] = __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g));
-    }
-    bool bad = false;
-#pragma unroll
-    for (int g = 0; g < G; g++)
-      bad = bad || (g < it.cnt && (unsigned)it.pair[g] >= (unsigned)(a.nq * a.nprobe));
-    if (bad) {
-      if (lane == 0) atomicAdd(pl.err, 1);
-      it.cnt = 0;
-#pragma unroll
-      for (int g = 0; g < G; g++) it.pair[g] = 0;
-    }
-#pragma unroll
-    for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
-  };
-  // loader wave 8: take the next item and stage its record words in slot sl
-  auto take = [&](int sl) __attribute__((always_inline)) {
-    int e = 0;
-    if (lane == 0) e = atomicAdd(pl.hdr + 2, 1);
-    e = __builtin_amdgcn_readfirstlane(e);
-    if (e < n_items) {
-      const int rv = fused_record(a, pl, nloc, e, n_items0, s_ex[0], s_ex[1], s_ord, G, lane);
-      if (lane < 16) s_rec[sl][lane] = rv;
-    }
-    if (lane == 0) s_idx[sl] = e < n_items ? e : -1;
-  };
-  // loader waves: item of slot sl -> LUT buffer b (T1 - 2 T3 or -T3, 4 pairs interleaved), its bounds
-  auto build = [&](int sl, int b) __attribute__((always_inline)) {
-    Item<G> it;
-    unpack(it, s_rec[sl][lane & 15]);
-    const int ltid = tid - 64 * kPipeScan;
-    if (ltid < G) {
-      int q = it.q[0];
-#pragma unroll
-      for (int g = 1; g < G; g++) q = ltid == g ? it.q[g] : q;
-      s_tq[b][ltid] = tau_get(pl, q);
-      s_wb[b][ltid] = f2ord(kInf);
-    }
-    const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)it.q[0] * LUTN
-                                                           : a.T1 + (int64_t)it.l * LUTN);
-    // rows in groups of NVG (40 staging VGPRs at NVG = 2): the loaders have a whole
-    // scan phase for the round trips, the registers are the scarcer resource
-    constexpr int NVG = NV < 2 ? NV : 2;
-#pragma unroll
-    for (int e0 = 0; e0 < NV; e0 += NVG) {
-      float4 b1[NVG], b3[NVG][G];
-#pragma unroll
-      for (int e = 0; e < NVG; e++) {
-        const int v = (e0 + e) * 256 + ltid;
-        b1[e] = T1l[v];
-#pragma unroll
-        for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN)[v];
-      }
-#pragma unroll
-      for (int e = 0; e < NVG; e++) {
-        const int v = (e0 + e) * 256 + ltid;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          float4 o;
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            const float x3 = comp(b3[e][g], c);
-            const float lv = ip ? -x3 : __builtin_fmaf(x3, -2.0f, comp(b1[e], c));  // (as k_scan_lists)
-            setc(o, g, lv);
-          }
-          lut[b][4 * v + c] = o;
-        }
-      }
-    }
-  };
-
-  // prologue: items 0 and 1 staged, item 0 built
-  if (wave == kPipeScan) {
-    take(0);
-    take(1);
-  }
-  __syncthreads();
-  if (!(wave < kPipeScan) && s_idx[0] >= 0) build(0, 0);
-  __syncthreads();
-
-  // scan-wave state carried across items
-  CodeWords<M> cw[JB];
-  bool have_codes = false;  // cw holds this item's first step (loaded before the barrier)
-  uint64_t prev_rk = kKcNone;
-  int prev_cnt = 0, prev_pair[G];
-  int64_t prev_beg = 0;
-#pragma unroll
-  for (int g = 0; g < G; g++) prev_pair[g] = 0;
-
-  for (int P = 0;; P++) {
-    const int sl = P % 3, b = P & 1;
-    if (wave == 0) PDIAG(0, __builtin_amdgcn_s_memtime());
-    // waves 0..3: the previous item's partial lists (own rows merged with wave w + 4's)
-    if (wave < 4 && prev_cnt > 0) {
-      const uint64_t c = s_rows[b ^ 1][wave][lane];
-      const uint64_t rv = ((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(c >> 32)) << 32) |
-                          (uint32_t)rev16_i((int)(uint32_t)c);
-      uint64_t q = rv < prev_rk ? rv : prev_rk;
-      kc_steps<128, 8>(q, lane);
-      const int rg = lane >> 4, re = lane & 15;
-      int pr = prev_pair[0];
-#pragma unroll
-      for (int g = 1; g < G; g++) pr = rg == g ? prev_pair[g] : pr;
-      if (rg < prev_cnt && re < k) {
-        const int64_t o = ((int64_t)pr * 4 + wave) * pl.ks + re;
-        const bool empty = q == kKcNone;
-        pl.partD[o] = empty ? FLT_MAX : kc_key(q);
-        pl.partI[o] = empty ? -1 : prev_beg + (int64_t)(uint32_t)q;
-      }
-    }
-    prev_cnt = 0;
-    if (s_idx[sl] < 0) break;  // workgroup-uniform (LDS, written before the last barrier)
-
-    if (!(wave < kPipeScan)) {
-      // ---------------------------------------------------------------- loaders
-      if (wave == kPipeScan) take((P + 2) % 3);
-      if (wave == kPipeScan) PDIAG(1, __builtin_amdgcn_s_memtime());
-      if (s_idx[(P + 1) % 3] >= 0) build((P + 1) % 3, b ^ 1);
-      PDIAG_WAIT();
-      if (wave == kPipeScan) PDIAG(2, __builtin_amdgcn_s_memtime());
-      if (wave == kPipeScan + 1) PDIAG(3, __builtin_amdgcn_s_memtime());
-    } else {
-      // ------------------------------------------------------------- scanners
-      Item<G> it;
-      unpack(it, s_rec[sl][lane & 15]);
-      const int n = it.n;
-      const uint8_t* lc = a.codes + it.beg * M;
-      if (wave == 0) PDIAG(13, __builtin_amdgcn_s_memtime());
-      if (wave == 0) PDIAG(12, (uint64_t)n | ((uint64_t)it.cnt << 32) | ((uint64_t)it.kind << 40));
-      int qix[G];
-      float bound[G];
-      bool loose = false;
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        qix[g] = it.q[g];
-        bound[g] = g < it.cnt ? ord2f(s_tq[b][g]) : -kInf;
-        loose = loose || bound[g] == kInf;
-      }
-      uint64_t rk = kKcNone;  // row g = pair g's sorted top-16
-      uint64_t rtp[G];        // pair g's k-th word (admission threshold)
-      int qn[G];
-#pragma unroll
-      for (int g = 0; g < G; g++) {
-        rtp[g] = kKcNone;
-        qn[g] = 0;
-      }
-      auto drain = [&]() __attribute__((always_inline)) {
-        int qmax = 0;
-#pragma unroll
-        for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
-        const int rg = lane >> 4, re = lane & 15;
-        int qr = qn[0];
-#pragma unroll
-        for (int g = 1; g < G; g++) qr = rg == g ? qn[g] : qr;
-        uint64_t thr = rtp[0];
-#pragma unroll
-        for (int g = 1; g < G; g++) thr = rg == g ? rtp[g] : thr;
-        for (int b0 = 0; b0 < qmax; b0 += 16) {
-          const int e = b0 + re;
-          uint64_t c = e < qr ? pack_kc(qd[wave][rg * QG + e], qi[wave][rg * QG + e]) : kKcNone;
-          c = c < thr ? c : kKcNone;
-          if (__builtin_amdgcn_ballot_w64(c != kKcNone) == 0) continue;
-          kc_steps<2, 1>(c, lane);
-          kc_steps<4, 2>(c, lane);
-          kc_steps<8, 4>(c, lane);
-          kc_steps<128, 8>(c, lane);
-          const uint64_t rv = ((uint64_t)(uint32_t)rev16_i((int)(uint32_t)(c >> 32)) << 32) |
-                              (uint32_t)rev16_i((int)(uint32_t)c);
-          uint64_t q = rv < rk ? rv : rk;
-          kc_steps<128, 8>(q, lane);
-          rk = q;
-#pragma unroll
-          for (int g = 0; g < G; g++) rtp[g] = readlane_u64(rk, 16 * g + k - 1);
-          thr = rtp[0];
-#pragma unroll
-          for (int g = 1; g < G; g++) thr = rg == g ? rtp[g] : thr;
-        }
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          bound[g] = fminf(bound[g], rtp[g] == kKcNone ? kInf : kc_key(rtp[g]));
-          qn[g] = 0;
-        }
-        loose = false;
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          loose = loose || bound[g] == kInf;
-          if (g < it.cnt && rtp[g] != kKcNone && lane == 0) {
-            atomicMin(&s_wb[b][g], f2ord(kc_key(rtp[g])));
-            tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
-          }
-        }
-      };
-
-      for (int sb = 0; sb < n; sb += CH * JB) {
-        if (sb > 0 || !have_codes) {
-#pragma unroll
-          for (int j = 0; j < JB; j++) {
-            const int i = sb + j * CH + wave * 64 + lane;
-            cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
-          }
-        }
-        const int tn = min(JB, (n - sb + CH - 1) / CH);  // chunk steps with codes (wave-uniform)
-        const bool last_sb = sb + CH * JB >= n;
-        float dis[JB][G];
-#pragma unroll
-        for (int jd = 0; jd < JB / 2; jd++) {
-          if (2 * jd < tn) {
-            CodeWords<M> cc[2] = {cw[2 * jd], cw[2 * jd + 1]};
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-#pragma unroll
-              for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(cc[h].w[v]));
-#pragma unroll
-            for (int h = 0; h < 2; h++)
-#pragma unroll
-              for (int g = 0; g < G; g++) dis[2 * jd + h][g] = it.d0[g];
-#pragma unroll
-            for (int m = 0; m < M; m++) {
-#pragma unroll
-              for (int h = 0; h < 2; h++) {
-                const float4 v = lut[b][m * 256 + cc[h].byte(m)];
-#pragma unroll
-                for (int g = 0; g < G; g++) dis[2 * jd + h][g] = dis[2 * jd + h][g] + comp(v, g);
-              }
-            }
-          }
-        }
-        // a query without a bound gets one from this step: the k-th smallest of
-        // the 64 lane minima (k distinct codes) bounds the final k-th key
-        if (loose) {
-#pragma unroll
-          for (int g = 0; g < G; g++) {
-            if (bound[g] != kInf) continue;  // wave-uniform
-            float mn = kInf;
-#pragma unroll
-            for (int j = 0; j < JB; j++)
-              if (j < tn && sb + j * CH + wave * 64 + lane < n) mn = fminf(mn, dis[j][g]);
-            const float T = wave_kth_smallest(mn, k, lane);
-            if (T < kInf && lane == 0) {
-              atomicMin(&s_wb[b][g], f2ord(T));
-              tau_lower(pl, qix[g], f2ord(T));
-            }
-          }
-        }
-        loose = false;
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[b][g]));
-          loose = loose || bound[g] == kInf;
-        }
-        int t = 0;
-        bool pend = false;
-        uint32_t bits = 0;
-#pragma unroll
-        for (int j = 0; j < JB; j++) {
-          if (j < tn) {
-            const bool valid = sb + j * CH + wave * 64 + lane < n;
-#pragma unroll
-            for (int g = 0; g < G; g++) bits |= (uint32_t)(valid && dis[j][g] <= bound[g]) << (j * G + g);
-          }
-        }
-        if (__builtin_amdgcn_ballot_w64(bits != 0) == 0) {
-          t = tn;
-        } else if (!loose) {
-          const int c = __popc(bits);
-          int tot = 0;
-#pragma unroll
-          for (int bb = 0; bb < 5; bb++) tot += __popcll(__builtin_amdgcn_ballot_w64((c >> bb) & 1)) << bb;
-          int qmax = 0;
-#pragma unroll
-          for (int g = 0; g < G; g++) qmax = max(qmax, qn[g]);
-          if (qmax + tot <= QG) {  // slots from a packed per-pair prefix sum (as k_scan_lists)
-            uint32_t cp = 0;
-#pragma unroll
-            for (int g = 0; g < G; g++) {
-              uint32_t cg = 0;
-#pragma unroll
-              for (int j = 0; j < JB; j++) cg += (bits >> (j * G + g)) & 1u;
-              cp |= cg << (8 * g);
-            }
-            const uint32_t incl = wave_incl_scan_u32(cp, lane);
-            const uint32_t totp = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            const uint32_t at = incl - cp;
-            int off[G];
-#pragma unroll
-            for (int g = 0; g < G; g++) off[g] = g * QG + qn[g] + (int)((at >> (8 * g)) & 0xffu);
-#pragma unroll
-            for (int j = 0; j < JB; j++) {
-#pragma unroll
-              for (int g = 0; g < G; g++) {
-                if ((bits >> (j * G + g)) & 1u) {
-                  qd[wave][off[g]] = dis[j][g];
-                  qi[wave][off[g]] = sb + j * CH + wave * 64 + lane;
-                  off[g]++;
-                }
-              }
-            }
-#pragma unroll
-            for (int g = 0; g < G; g++) qn[g] += (int)((totp >> (8 * g)) & 0xffu);
-            t = tn;
-          }
-        }
-        while (t < tn) {
-          int stop = tn;
-          bool want = false;
-          bool go = true;
-#pragma unroll
-          for (int j = 0; j < JB; j++) {
-            if (go && j >= t && j < tn) {
-              const int i = sb + j * CH + wave * 64 + lane;
-              const bool valid = i < n;
-              uint64_t mk[G];
-              int tj = 0;
-#pragma unroll
-              for (int g = 0; g < G; g++) {
-                mk[g] = __builtin_amdgcn_ballot_w64(valid && dis[j][g] <= bound[g]);
-                tj += __popcll(mk[g]);
-              }
-              bool full = false;
-#pragma unroll
-              for (int g = 0; g < G; g++) full = full || qn[g] + __popcll(mk[g]) > QG;
-              if (tj > 0) {
-                if (full) {
-                  stop = j;
-                  want = true;
-                  go = false;
-                } else {
-#pragma unroll
-                  for (int g = 0; g < G; g++) {
-                    if ((mk[g] >> lane) & 1) {
-                      const int q = g * QG + qn[g] + __popcll(mk[g] & lanemask_lt);
-                      qd[wave][q] = dis[j][g];
-                      qi[wave][q] = i;
-                    }
-                    qn[g] += __popcll(mk[g]);
-                  }
-                  if (loose) {
-                    stop = j + 1;
-                    want = true;
-                    go = false;
-                  }
-                }
-              }
-            }
-          }
-          if (stop >= tn) {
-            pend = want;
-            break;
-          }
-          drain();
-          t = stop;
-        }
-        bool queued = false;
-#pragma unroll
-        for (int g = 0; g < G; g++) queued = queued || qn[g] > 0;
-        if (pend || (last_sb && queued)) drain();
-      }
-      // the next item's first codes, in flight across the barrier (its record was
-      // staged a phase ago)
-      have_codes = false;
-      const int ns = (P + 1) % 3;
-      if (s_idx[ns] >= 0) {
-        const int w2 = s_rec[ns][2], w3 = s_rec[ns][3], w4 = s_rec[ns][4];
-        const int n2 = w2 - w3;
-        const uint8_t* lc2 = a.codes + (int64_t)(((uint64_t)(uint32_t)w4 << 32) | (uint32_t)w3) * M;
-#pragma unroll
-        for (int j = 0; j < JB; j++) {
-          const int i = j * CH + wave * 64 + lane;
-          cw[j].load(lc2 + (int64_t)(i < n2 ? i : 0) * M);
-        }
-        have_codes = true;
-      }
-      PDIAG(4 + wave, __builtin_amdgcn_s_memtime());
-      if (wave >= 4) {
-        s_rows[b][wave - 4][lane] = rk;
-      } else {
-        prev_rk = rk;
-        prev_cnt = it.cnt;
-        prev_beg = it.beg;
-#pragma unroll
-        for (int g = 0; g < G; g++) prev_pair[g] = it.pair[g];
-      }
-    }
-    __syncthreads();  // item P scanned, item P + 1 built, item P + 2 staged
-  }
-}
-
-// Segmented coarse quantizer on 64-query tiles (k_coarse_segtop's output from the
-// tiled key GEMM): workgroup = 64 queries x one segment of centroids, walked in
-// tiles of 128; each tile's keys go to LDS (in the staging buffers), and wave w keeps
-// the nprobe best (key, list) words of queries 16 w .. 16 w + 15 in packed one-row
-// top-k lists.  Each centroid column is read from L2 once per 64 queries (4x fewer
-// than k_coarse_segtop); the keys are k_coarse_gemm's to the bit.
-constexpr int TKS = TC + 1;  // key tile row stride (floats)
-static_assert(TQ * TKS <= 2 * TKC * TBS, "the key tile fits the B staging buffers");
-__global__ __launch_bounds__(256) void k_coarse_segtop_tiled(const float* __restrict__ x, const float* __restrict__ xn,
-                                                             int64_t nq, int d, const float* __restrict__ centT,
-                                                             int ldc, const float* __restrict__ cn, int nlist, int ip,
-                                                             int seg, int nseg, int nprobe,
-                                                             uint64_t* __restrict__ cand) {
-  __shared__ __attribute__((aligned(16))) float As[2][TQ * TAS];
-  __shared__ __attribute__((aligned(16))) float Bs[2][TKC * TBS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t q0 = (int64_t)(blockIdx.x / nseg) * TQ;
-  const int sg = blockIdx.x % nseg;
-  const int cb = sg * seg, ce = min(nlist, cb + seg);
-  const int i16 = lane & 15, k4 = lane >> 4;
-  float* kt = &Bs[0][0];  // [TQ][TKS] keys of the current tile
-  PackedTopK<1> tk[16];   // queries 16 wave .. 16 wave + 15
-#pragma unroll
-  for (int u = 0; u < 16; u++) tk[u].init(nprobe);
-  float xq[4];  // |x|^2 of this lane's 4 accumulator rows
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int64_t q = q0 + wave * 16 + k4 * 4 + r;
-    xq[r] = (ip || q >= nq) ? 0.f : xn[q];
-  }
-  for (int c0 = cb; c0 < ce; c0 += TC) {
-    f4 acc[TC / 16];
-    tiled_key_acc(acc, x, q0, nq, d, centT, ldc, c0, As, Bs, tid);
-#pragma unroll
-    for (int t = 0; t < TC / 16; t++) {
-      const int c = c0 + t * 16 + i16;
-      const float cnv = ip ? 0.f : cn[min(c, nlist - 1)];
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        kt[(wave * 16 + k4 * 4 + r) * TKS + t * 16 + i16] = coarse_key(acc[t][r], xq[r], cnv, ip);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const float* kr = kt + (wave * 16 + u) * TKS;
-#pragma unroll
-      for (int h = 0; h < TC / 64; h++) {
-        const int c = c0 + h * 64 + lane;
-        const uint64_t p = c < ce ? pack_kc(kr[h * 64 + lane], c) : kKcNone;
-        const bool pass = p < tk[u].tp;
-        const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
-        if (!mk) continue;  // wave-uniform
-        if (__popcll(mk) > 4)
-          kc_bulk_merge(tk[u], pass ? p : kKcNone, lane);
-        else
-          tk[u].insert(mk, p, lane);
-      }
-    }
-    __syncthreads();  // the keys are read before the next tile's staging overwrites them
-  }
-#pragma unroll
-  for (int u = 0; u < 16; u++) {
-    const int64_t q = q0 + wave * 16 + u;
-    if (q < nq && lane < nprobe) cand[(q * nseg + sg) * nprobe + lane] = tk[u].p[0];
   }
 }
 
@@ -3224,12 +2498,7 @@ __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__
   };
   for (int t0 = cb; t0 < ce; t0 += GC) {
     f4 acc[NTL];
-#ifdef SEGTOP_NOMMA  // timing experiment only (wrong results): no key tiles
-#pragma unroll
-    for (int t = 0; t < NTL; t++) acc[t] = f4{(float)t0, 1.f, 2.f, 3.f};
-#else
     coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, t0 + wave * 32, lane);
-#endif
     __syncthreads();  // xn (first tile); the previous tile's keys have been read
 #pragma unroll
     for (int t = 0; t < NTL; t++) {
@@ -3242,9 +2511,6 @@ __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__
       }
     }
     __syncthreads();
-#ifdef SEGTOP_NOSEL  // timing experiment only (wrong results): no selection
-    if (t0 >= 0) continue;
-#endif
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int i = wave * 4 + u;
@@ -3304,28 +2570,114 @@ __global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __re
   coarse_emit(tk.p[0], q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
 }
 
+// ---- stale partial lists: accounting, event log, repair
+// hdr[kHdrStale] counts (query, merge launch) pairs that read an entry whose tag
+// was not this batch's, hdr[kHdrRepair] the probes k_merge_probes rescanned, and
+// hdr[kHdrLog] the events offered to the log (the first kEvLog are kept:
+// ListPlan::evlog, 8 words each -- site | reader XCD << 8, query, list j | rank
+// << 16, expected tag, found tag, found key bits, epoch, and the system-scope
+// re-read result: the reads until the tag was fresh (full merge), or 0xFFFFFFFF
+// when it never was within kSpin reads).
+__device__ __forceinline__ int log_slot(const ListPlan& pl) {
+  const int e = atomicAdd(pl.hdr + kHdrLog, 1);
+  return e < kEvLog ? e : -1;
+}
+__device__ __forceinline__ void log_stale(const ListPlan& pl, int e, int site, int64_t q, int j, int i, uint32_t expect,
+                                          uint32_t found, uint32_t keyb, uint32_t spin) {
+  uint32_t* r = pl.evlog + 8 * e;
+  r[0] = (uint32_t)site | (xcc_tag() >> 20);
+  r[1] = (uint32_t)q;
+  r[2] = (uint32_t)j | ((uint32_t)i << 16);
+  r[3] = expect;
+  r[4] = found;
+  r[5] = keyb;
+  r[6] = pl.epoch;
+  r[7] = spin;
+}
+// re-read a stale record's (key, tag) word at system scope until its tag is
+// fresh: the number of reads it took, or 0xFFFFFFFF (never, within kSpin)
+constexpr int kSpin = 2000;
+__device__ __forceinline__ uint32_t spin_fresh(const uint4* rec, uint32_t expect) {
+  for (int t = 0; t < kSpin; t++) {
+    const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(rec), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tag_ok((uint32_t)(v >> 32), expect)) return (uint32_t)t + 1;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  return 0xFFFFFFFFu;
+}
+
+// Rescan probe p of query q from the index itself -- the list's codes, the
+// query's T3 row and the list's T1 row, with the scan's arithmetic (LUT entry
+// fma(T3, -2, T1) or -T3, dis0 + sum over m in order), so every key is the
+// scan's to the bit -- and merge every code of the list into tk by (key, label),
+// skipping entries tk already holds (a partial list can be stale from some rank
+// on, after its fresh prefix was merged).  One wave; rare (the stale-list path).
+template <int R>
+__device__ __forceinline__ void repair_probe(const ScanArgs& a, const ListPlan& pl, int64_t q, int p, WaveTopK<R>& tk,
+                                          int lane) {
+  const int64_t pair = q * a.nprobe + p;
+  const int64_t l = a.probe_list[pair];
+  const int64_t beg = a.list_off[l], n = a.list_off[l + 1] - beg;
+  const float d0 = pl.pd0[pair];
+  const int M = a.M;
+  const float* T3q = a.T3 + q * (int64_t)M * 256;
+  const float* T1l = a.ip ? T3q : a.T1 + l * (int64_t)M * 256;
+  for (int64_t i0 = 0; i0 < n; i0 += 64) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < n;
+    const int64_t pos = beg + (valid ? i : 0);
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(a.codes + pos * M);
+    float key = d0;
+    for (int m4 = 0; m4 < M / 4; m4++) {
+      const uint32_t w = cw[m4];
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int e = (m4 * 4 + b) * 256 + (int)((w >> (8 * b)) & 255u);
+        const float x3 = T3q[e];
+        const float lv = a.ip ? -x3 : __builtin_fmaf(x3, -2.0f, T1l[e]);
+        key = key + lv;
+      }
+    }
+    const int64_t id = valid ? a.ids[pos] : kSentinelId;
+    uint64_t mask = __builtin_amdgcn_ballot_w64(valid && lexless(key, id, tk.td, tk.ti));
+    while (mask) {
+      const int src = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float vd = readlane_f(key, src);
+      const int64_t vi = id_readlane(id, src);
+      bool dup = false;
+#pragma unroll
+      for (int r = 0; r < R; r++) dup = dup || __builtin_amdgcn_ballot_w64(tk.d[r] == vd && tk.id[r] == vi) != 0;
+      if (!dup) tk.insert(1ull << src, key, id, lane);
+    }
+  }
+}
+
 // Per query (one wave): merge the per-wave partial lists of every scanned
-// probe ([probe][4 waves][k], sorted by (key, position)).  All entries are
-// fetched in batches of 64 lanes x B loads (one round trip per batch); labels
-// are looked up only for entries that can still enter the top-k.
+// probe ([probe][4 waves][k] tagged records, sorted by (key, position)).  All
+// entries are fetched in batches of 64 lanes x B loads (one round trip per
+// batch); labels are looked up only for entries that can still enter the top-k.
+// An entry whose tag is not this batch's is never used: its probe is rescanned
+// (repair_probe) after the other lists are merged.
 template <int R>
 __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   constexpr int B = 4;
+  __shared__ uint64_t s_bad[4][kMaxK / 64];  // per wave: the probes with a stale entry (full merge)
   const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   if (blockIdx.x == 0) {  // the scan consumed the counts and its work counter: zero them for the next batch
     const int nloc = a.list_hi - a.list_lo;
     for (int i = threadIdx.x; i < 2 * nloc; i += 256) pl.cnt[i] = 0;
     if (threadIdx.x == 0) pl.hdr[2] = 0;
-#ifdef ORDER_CANARY
-    if (threadIdx.x == 0) pl.hdr[13] = 0;
-#endif
   }
-  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave;
   if (q >= a.nq) return;
   const int k = a.k;
   const int np = a.nprobe;
   const float pad = a.ip ? -FLT_MAX : FLT_MAX;
   const float sgn = a.ip ? -1.f : 1.f;  // key -> reported value
+  const int64_t ks = pl.ks;
   if (R == 1 && np * 4 <= 64) {
     // fast path: lane j owns partial list j = (probe j/4, wave j%4), sorted by
     // (key, label).  T = the k-th smallest list head bounds the k-th key (k
@@ -3334,57 +2686,76 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     // looked up, and one 64-lane sort yields the top-k.
     __shared__ float sd[4][64];
     __shared__ int64_t sp[4][64];
-    const int wave = threadIdx.x >> 6;
     constexpr int U = 16;
     float d[U];
     const int p = min(lane >> 2, np - 1);
     // the planner's mask of the probes the scan covered (empty or foreign lists are not)
     const bool scanned = (lane >> 2) < np && ((pl.qmask[q] >> p) & 1);
-    const int64_t base = ((q * np + p) * 4 + (lane & 3)) * pl.ks;
+    const int64_t slot = (q * np + p) * 4 + (lane & 3);
+    const uint32_t expect = part_tag(pl.epoch, slot);
     // unconditional, clamped loads (no divergent branch around them); slots of
     // unscanned probes (empty or foreign lists, lanes past nprobe) were never
     // written this batch: their contents are stale and must not be used
     int64_t pos[U];
+    bool fresh[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      pos[u] = pl.partI[base + min(u, k - 1)];
-      d[u] = pl.partD[base + min(u, k - 1)];
+      const uint4 r = pl.part[slot * ks + min(u, k - 1)];
+      d[u] = rec_key(r);
+      pos[u] = rec_pos(r);
+      fresh[u] = tag_ok(r.y, expect);
     }
-    bool ok[U];
+    int bad_u = -1;
 #pragma unroll
-    for (int u = 0; u < U; u++) ok[u] = scanned && u < k && pos_ok(a, pl, pos[u]);
-    const float T = wave_kth_smallest(ok[0] ? d[0] : kInf, k, lane);
-    const uint64_t lt = (1ull << lane) - 1;
-    int total = 0;
+    for (int u = U - 1; u >= 0; u--) bad_u = (scanned && u < k && !fresh[u]) ? u : bad_u;
+    if (__builtin_amdgcn_ballot_w64(bad_u >= 0)) {  // stale entries: the full merge below re-reads and repairs
+      if (lane == (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(bad_u >= 0))) atomicAdd(pl.hdr + kHdrStale, 1);
+      if (bad_u >= 0) {
+        const int ev = log_slot(pl);
+        if (ev >= 0) {  // (and whether an immediate system-scope re-read is already fresh)
+          const uint4 r = pl.part[slot * ks + bad_u];
+          log_stale(pl, ev, 1, q, lane, bad_u, expect, r.y, r.x,
+                    spin_fresh(pl.part + slot * ks + bad_u, expect) == 1 ? 1u : 0u);
+        }
+      }
+    } else {
+      bool ok[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const bool pass = ok[u] && d[u] <= T;
-      const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
-      const int at = total + __popcll(mk & lt);
-      if (pass && at < 64) {
-        sd[wave][at] = d[u];
-        sp[wave][at] = pos[u];
+      for (int u = 0; u < U; u++) ok[u] = scanned && u < k && pos_ok(a, pl, pos[u]);
+      const float T = wave_kth_smallest(ok[0] ? d[0] : kInf, k, lane);
+      const uint64_t lt = (1ull << lane) - 1;
+      int total = 0;
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const bool pass = ok[u] && d[u] <= T;
+        const uint64_t mk = __builtin_amdgcn_ballot_w64(pass);
+        const int at = total + __popcll(mk & lt);
+        if (pass && at < 64) {
+          sd[wave][at] = d[u];
+          sp[wave][at] = pos[u];
+        }
+        total += __popcll(mk);
       }
-      total += __popcll(mk);
-    }
-    // a list whose 16 loaded entries all pass may hold more candidates
-    const bool cut = k > U && __builtin_amdgcn_ballot_w64(ok[U - 1] && d[U - 1] <= T) != 0;
-    if (T < kInf && total <= 64 && !cut) {
-      __builtin_amdgcn_wave_barrier();
-      float cd = lane < total ? sd[wave][lane] : kInf;
-      int64_t ci = lane < total ? a.ids[sp[wave][lane]] : kSentinelId;
-      bitonic_sort64<2>(cd, ci, lane);
-      if (lane < k) {
-        const bool empty = ci == kSentinelId;
-        a.outD[q * k + lane] = empty ? pad : sgn * cd;
-        a.outI[q * k + lane] = empty ? -1 : ci;
+      // a list whose 16 loaded entries all pass may hold more candidates
+      const bool cut = k > U && __builtin_amdgcn_ballot_w64(ok[U - 1] && d[U - 1] <= T) != 0;
+      if (T < kInf && total <= 64 && !cut) {
+        __builtin_amdgcn_wave_barrier();
+        float cd = lane < total ? sd[wave][lane] : kInf;
+        int64_t ci = lane < total ? a.ids[sp[wave][lane]] : kSentinelId;
+        bitonic_sort64<2>(cd, ci, lane);
+        if (lane < k) {
+          const bool empty = ci == kSentinelId;
+          a.outD[q * k + lane] = empty ? pad : sgn * cd;
+          a.outI[q * k + lane] = empty ? -1 : ci;
+        }
+        return;
       }
-      return;
     }
   }
   if constexpr (R >= 2) {
-    // k > 64, nprobe <= 64: k_merge_big ran first and merged every query whose
-    // candidates fit its buffer; the rest (ties) take the full merge below
+    // k > 64, nprobe <= 64: k_merge_radix / k_merge_big ran first and merged every
+    // query whose candidates fit their buffers and whose lists were all fresh;
+    // the rest (ties, stale entries) take the full merge below
     if (np <= 64) {
       const int done = pl.qdone[q];
       __builtin_amdgcn_wave_barrier();
@@ -3397,12 +2768,15 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   // i + 1, ...), so the running k-th key falls fast and few labels are looked
   // up; once a batch of at least L consecutive entries (one per list) admits
   // nothing, no later entry of any list can (each list is ascending and the
-  // k-th key only falls).
+  // k-th key only falls).  Stale entries mark their probe in s_bad.
+  if (lane < kMaxK / 64) s_bad[wave][lane] = 0;
+  __builtin_amdgcn_wave_barrier();
   WaveTopK<R> tk;
   tk.init(k);
   const int L = 4 * np;
   const int total = L * k;
-  const int64_t qbase = q * (int64_t)L * pl.ks;
+  const int qmw = pl.qmw;
+  bool stale = false;
   for (int e0 = 0; e0 < total; e0 += 64 * B) {
     float d[B];
     int64_t pos[B];
@@ -3416,18 +2790,38 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
         const int i = R == 1 ? e % k : e / L;
         const int j = R == 1 ? e / k : e - (e / L) * L;  // rank i of list j = (probe j / 4, wave j % 4)
         const int p = j >> 2;
-        bool scanned;
-        if (np <= 64) {
-          scanned = (pl.qmask[q] >> p) & 1;
-        } else {
-          const int64_t l = a.probe_list[q * np + p];
-          scanned = l >= a.list_lo && l < a.list_hi && a.list_off[l + 1] > a.list_off[l];
+        const bool scanned = (pl.qmask[q * qmw + (p >> 6)] >> (p & 63)) & 1;
+        const int64_t slot = q * (int64_t)L + j;
+        const uint32_t expect = part_tag(pl.epoch, slot);
+        bool bad = false;
+        if (scanned) {
+          // k > 64 writes only each list's valid prefix ((count, tag) in partN)
+          int nv = k;
+          if (R >= 2) {
+            const uint2 nt = pl.partN[slot];
+            if (tag_ok(nt.y, expect)) nv = (int)nt.x;
+            else bad = true;
+            const int ev = (bad && i == 0) ? log_slot(pl) : -1;
+            if (ev >= 0)
+              log_stale(pl, ev, 2, q, j, 0xFFFF, expect, nt.y, nt.x,
+                        spin_fresh(reinterpret_cast<const uint4*>(pl.partN + slot), expect));
+          }
+          if (!bad && i < nv) {
+            const uint4* rp = pl.part + slot * ks + i;
+            const uint4 r = *rp;
+            if (tag_ok(r.y, expect)) {
+              d[b] = rec_key(r);
+              pos[b] = rec_pos(r);
+            } else {
+              bad = true;
+              const int ev = log_slot(pl);
+              if (ev >= 0) log_stale(pl, ev, 2, q, j, i, expect, r.y, r.x, spin_fresh(rp, expect));
+            }
+          }
         }
-        // k > 64 writes only each list's valid prefix (partN entries)
-        if (scanned && (R == 1 || i < pl.partN[q * (int64_t)L + j])) {
-          const int64_t at = qbase + (int64_t)j * pl.ks + i;
-          d[b] = pl.partD[at];
-          pos[b] = pl.partI[at];
+        if (bad) {
+          atomicOr(reinterpret_cast<unsigned long long*>(&s_bad[wave][p >> 6]), 1ull << (p & 63));
+          stale = true;
         }
       }
     }
@@ -3451,6 +2845,19 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
         continue;
       }
       tk.insert(mask, d[b], id, lane);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(stale)) {  // (wave-uniform) rescan every probe with a stale entry
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+    for (int w = 0; w < (np + 63) / 64; w++) {
+      uint64_t m = s_bad[wave][w];
+      while (m) {
+        const int p = w * 64 + (int)__builtin_ctzll(m);
+        m &= m - 1;
+        repair_probe<R>(a, pl, q, p, tk, lane);
+        if (lane == 0) atomicAdd(pl.hdr + kHdrRepair, 1);
+      }
     }
   }
 #pragma unroll
@@ -3496,19 +2903,37 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   const int64_t qb = q * (int64_t)L;  // list j: entries at (qb + j) * k + i
   const float pad = a.ip ? -FLT_MAX : FLT_MAX;
   const float sgn = a.ip ? -1.f : 1.f;
-  auto key_at = [&](int j, int i) __attribute__((always_inline)) { return pl.partD[(qb + j) * pl.ks + i]; };
+  // every record and count read is tag-checked: a stale one sends the query to
+  // k_merge_probes' full merge (which rescans its probe) instead of being used
+  bool stale = false;
+  auto key_at = [&](int j, int i) __attribute__((always_inline)) {
+    const uint2 v = *reinterpret_cast<const uint2*>(pl.part + (qb + j) * pl.ks + i);
+    stale = stale || !tag_ok(v.y, part_tag(pl.epoch, qb + j));
+    return __uint_as_float(v.x);
+  };
 
   int C = 0;
 #pragma unroll
   for (int t = 0; t < 4; t++) {
     const int j = t * 64 + lane;
-    int n = (j < L && ((qm >> (j >> 2)) & 1)) ? pl.partN[qb + j] : 0;
-    if (n < 0 || n > k) {  // a partial list holds at most k entries
-      atomicAdd(pl.err, 1);
-      n = 0;
+    int n = 0;
+    if (j < L && ((qm >> (j >> 2)) & 1)) {
+      const uint2 nt = pl.partN[qb + j];
+      n = (int)nt.x;
+      if (!tag_ok(nt.y, part_tag(pl.epoch, qb + j))) {
+        stale = true;
+        n = 0;
+      } else if (n < 0 || n > k) {  // a partial list holds at most k entries
+        atomicAdd(pl.err, 1);
+        n = 0;
+      }
     }
     lens[j] = n;
     C += n;
+  }
+  if (__builtin_amdgcn_ballot_w64(stale)) {  // (uniform)
+    if (lane == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+    return;
   }
   C = wave_sum_i(C);
   __builtin_amdgcn_wave_barrier();
@@ -3606,11 +3031,16 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
           const int mid = (lo + hi) >> 1;
           if (sp[mid] <= e) lo = mid; else hi = mid;
         }
-        const int64_t at = (qb + lo) * pl.ks + (e - sp[lo]);
-        cd[e] = pl.partD[at];
-        cl[e] = pl.partI[at];
+        const uint4 r = pl.part[(qb + lo) * pl.ks + (e - sp[lo])];
+        stale = stale || !tag_ok(r.y, part_tag(pl.epoch, qb + lo));
+        cd[e] = rec_key(r);
+        cl[e] = rec_pos(r);
       }
     }
+  }
+  if (__builtin_amdgcn_ballot_w64(stale)) {  // (uniform)
+    if (lane == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+    return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -3715,19 +3145,8 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
 // Queries whose ties overflow kRadixCap are left to k_merge_probes' full merge.
 constexpr int kRadixU = 32;
 constexpr int kRadixCap = 512;
-#ifndef MERGE_RADIX
-#define MERGE_RADIX 1  // -DMERGE_RADIX=0: k_merge_big for every k > 64 (A/B variant)
-#endif
 
 __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
-#ifdef MERGE_ACQ
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // A/B: coherence experiment
-#endif
-#ifdef ORDER_CANARY
-  // every list-scan workgroup of this batch must have exited before this launch
-  if (threadIdx.x == 0 && __hip_atomic_load(pl.hdr + 13, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != pl.grid)
-    atomicAdd(pl.err, 1000);
-#endif
   __shared__ int s_len[256];
   __shared__ int s_hist[256];
   __shared__ int s_wsum[4];
@@ -3743,11 +3162,18 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
   const float pad = a.ip ? -FLT_MAX : FLT_MAX;
   const float sgn = a.ip ? -1.f : 1.f;
   const uint64_t lt = (1ull << lane) - 1;
+  // every count and record read is tag-checked: a stale one sends the query to
+  // k_merge_probes' full merge (which rescans its probe) instead of being used
+  bool stale = false;
   {
     int n = 0;
     if (tid < L && ((qm >> (tid >> 2)) & 1)) {
-      n = pl.partN[qb + tid];
-      if (n < 0 || n > k) {  // a partial list holds at most k entries
+      const uint2 nt = pl.partN[qb + tid];
+      n = (int)nt.x;
+      if (!tag_ok(nt.y, part_tag(pl.epoch, qb + tid))) {
+        stale = true;
+        n = 0;
+      } else if (n < 0 || n > k) {  // a partial list holds at most k entries
         atomicAdd(pl.err, 1);
         n = 0;
       }
@@ -3757,46 +3183,11 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     if (lane == 0) s_wsum[wave] = ws;
   }
   __syncthreads();
-#ifdef PART_CHECK
-  // experiment: each list as read here against (count, hash) as the scan wrote it;
-  // count mismatch -> +1000000, content mismatch -> +1000 in the error word
-  if (tid < L && ((qm >> (tid >> 2)) & 1)) {
-    const int64_t sl = qb + tid;
-    const uint32_t cn = __hip_atomic_load(pl.chk + 4 * sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t ch = __hip_atomic_load(pl.chk + 4 * sl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t cw = __hip_atomic_load(pl.chk + 4 * sl + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(pl.chk + 4 * sl + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cw != 1) atomicAdd(pl.err, 1000000);  // written by no item, or by more than one (as a count mismatch)
-    uint32_t h = 0;
-    for (int i = 0; i < s_len[tid]; i++)
-      h ^= part_hash(__float_as_uint(pl.partD[sl * pl.ks + i]), (uint32_t)pl.partI[sl * pl.ks + i], i);
-    if (cn != (uint32_t)s_len[tid]) {
-      atomicAdd(pl.err, 1000000);
-    } else if (h != ch) {
-      // re-read: agent-scope (L1 bypass) and system-scope loads; +100000 / +10000000 when
-      // those still differ from what the scan wrote
-      uint32_t h2 = 0, h3 = 0;
-      for (int i = 0; i < s_len[tid]; i++) {
-        const uint32_t kb = __hip_atomic_load(reinterpret_cast<const uint32_t*>(pl.partD) + sl * pl.ks + i,
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t pb = __hip_atomic_load(reinterpret_cast<const uint64_t*>(pl.partI) + sl * pl.ks + i,
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        h2 ^= part_hash(kb, (uint32_t)pb, i);
-        const uint32_t kb3 = __hip_atomic_load(reinterpret_cast<const uint32_t*>(pl.partD) + sl * pl.ks + i,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint64_t pb3 = __hip_atomic_load(reinterpret_cast<const uint64_t*>(pl.partI) + sl * pl.ks + i,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        h3 ^= part_hash(kb3, (uint32_t)pb3, i);
-      }
-      atomicAdd(pl.err, 1000 + (h2 != ch ? 100000 : 0) + (h3 != ch ? 10000000 : 0));
-    }
-  }
-#endif
   const int C = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
   const int ks = pl.ks;
   const int E = L * ks;
   const float inv_k = 1.0f / (float)ks;
-  const float* pd = pl.partD + qb * ks;
+  const uint4* pr = pl.part + qb * ks;
   uint32_t key[kRadixU];
 #pragma unroll
   for (int u = 0; u < kRadixU; u++) {
@@ -3804,13 +3195,17 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     key[u] = 0xFFFFFFFFu;  // absent (no finite key maps here)
     if (e < E) {
       const int j = div_small(e, ks, inv_k);
-      if (e - j * ks < s_len[j]) key[u] = ukey_of(pd[e]);
+      if (e - j * ks < s_len[j]) {
+        const uint2 v = *reinterpret_cast<const uint2*>(pr + e);  // (key, tag)
+        stale = stale || !tag_ok(v.y, part_tag(pl.epoch, qb + j));
+        key[u] = ukey_of(__uint_as_float(v.x));
+      }
     }
   }
-#if defined(RADIX_STOP) && RADIX_STOP == 1  // timing experiment only: stop after the key loads
-  if (key[0] == 0x12345u && key[kRadixU - 1] == 0x54321u) a.outD[0] = 0.f;
-  return;
-#endif
+  if (__syncthreads_or(stale)) {
+    if (tid == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+    return;
+  }
   // the k-th smallest present key (all of them when there are at most k)
   uint32_t T = 0xFFFFFFFEu;
   if (C > k) {
@@ -3864,14 +3259,9 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     }
     T = prefix;
   }
-#if defined(RADIX_STOP) && RADIX_STOP == 2  // ... after the radix select
-  if (T == 0x12345u) a.outD[0] = 0.f;
-  return;
-#endif
-  // compact the entries <= T (positions from partI)
+  // compact the entries <= T (records re-read whole: positions, and the tags checked again)
   if (tid == 0) s_n = 0;
   __syncthreads();
-  const int64_t* pi = pl.partI + qb * ks;
 #pragma unroll
   for (int u = 0; u < kRadixU; u++) {
     const bool c = key[u] <= T;  // (absent keys: 0xFFFFFFFF > T)
@@ -3883,16 +3273,18 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     const int at = base + (int)__popcll(mk & lt);
     if (c && at < kRadixCap) {
       const int e = u * 256 + tid;
-      cd[at] = pd[e];
-      cl[at] = pi[e];
+      const uint4 r = pr[e];
+      stale = stale || !tag_ok(r.y, part_tag(pl.epoch, qb + div_small(e, ks, inv_k)));
+      cd[at] = rec_key(r);
+      cl[at] = rec_pos(r);
     }
   }
-  __syncthreads();
+  if (__syncthreads_or(stale)) {
+    if (tid == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+    return;
+  }
   const int n = s_n;
   if (n > kRadixCap) return;  // ties overflow: the full merge of k_merge_probes takes this query
-#if defined(RADIX_STOP) && RADIX_STOP == 3  // ... after the compaction
-  return;
-#endif
   int P = 64;
   while (P < n) P <<= 1;
   for (int e = tid; e < P; e += 256) {
@@ -3905,9 +3297,6 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     }
   }
   __syncthreads();
-#if defined(RADIX_STOP) && RADIX_STOP == 4  // ... after the labels
-  return;
-#endif
   if (n <= 128 && k <= 128) {  // one wave sorts the candidates in registers (two 64-lane rows), no barriers
     if (wave == 0) {
       float d0 = lane < n ? cd[lane] : kInf, d1 = lane + 64 < n ? cd[lane + 64] : kInf;
@@ -4073,65 +3462,14 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
       attr_done |= 1ull << dev;
     }
   }
-#ifdef T3_MFMA  // A/B build: T3 on the matrix cores in its own launch (tolerance mode)
-  if (t3.nblk > 0 && (d / M) <= 16) {
-    hipLaunchKernelGGL(k_t3_mfma, dim3((unsigned)t3.nblk), dim3(256), 0, s, x, nq, d, cb, M, T3out);
-    t3.nblk = 0;
-  }
-#endif
   hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
                      (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
 }
 
-bool coarse_fused_ok(int nlist, int d, int nprobe) {
-  const size_t smem = sizeof(float) * ((size_t)((d + 63) & ~63) * GQ + GQ * 9 + (size_t)GQ * nlist);
-  return nlist <= kFusedCoarseLists && nprobe <= 64 && smem <= 150 * 1024;
-}
-
-void launch_coarse_fused(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist, int nprobe,
-                         float* out_dis, int64_t* out_list, hipStream_t s, bool ip, const ListPlan* plan,
-                         const int64_t* list_off, int lo, int hi, const float* cent, float* T3out, const float* cb,
-                         int M) {
-  if (nq <= 0) return;
-  const unsigned nkb = nblocks(nq, GQ);
-  CoarseT3 t3;
-  if (T3out && M > 0 && d % M == 0) {
-    t3.out = T3out;
-    t3.cb = cb;
-    t3.M = M;
-    t3.nblk = (int)(nkb * (unsigned)M);
-  }
-  const size_t smem = sizeof(float) * ((size_t)((d + 63) & ~63) * GQ + GQ * 9 + (size_t)GQ * nlist);
-  {  // dynamic LDS above 64 KiB is opted into per device
-    static uint64_t attr_done = 0;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 64 && !(attr_done & (1ull << dev))) {
-      (void)hipFuncSetAttribute((const void*)k_coarse_fused, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-      attr_done |= 1ull << dev;
-    }
-  }
-  CoarsePlan cp;
-  if (plan) {
-    cp.pl = *plan;
-    cp.on = 1;
-    cp.list_off = list_off;
-    cp.lo = lo;
-    cp.hi = hi;
-    cp.cent = cent;
-  }
-  hipLaunchKernelGGL(k_coarse_fused, dim3(nkb + (unsigned)t3.nblk), dim3(256), smem, s, x, nq, d, centT,
-                     (nlist + 3) & ~3, cn, nlist, ip ? 1 : 0, nprobe, out_dis, out_list, (int)nkb, t3, cp);
-}
-
-// the 64-query tiled form when the queries fill at least one tile and d % 4 == 0
-static bool segmented_tiled(int64_t nq, int d) { return TILED_SEGTOP && d % 4 == 0 && nq >= TQ; }
-
 int coarse_segments(int64_t nq, int nlist, int d) {
-  const bool tiled = segmented_tiled(nq, d);
-  const int64_t qt = tiled ? (nq + TQ - 1) / TQ : (nq + GQ - 1) / GQ;
-  const int tiles = (nlist + GC - 1) / GC;  // (TC == GC)
-  const int64_t min_wg = tiled ? 512 : 1024;  // two 54 KB workgroups per CU / four of k_coarse_segtop
+  const int64_t qt = (nq + GQ - 1) / GQ;
+  const int tiles = (nlist + GC - 1) / GC;
+  const int64_t min_wg = 1024;  // four k_coarse_segtop workgroups per CU
   const int want = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, (min_wg + qt - 1) / qt));
   const int seg = (tiles + want - 1) / want * GC;
   return (nlist + seg - 1) / seg;
@@ -4139,17 +3477,11 @@ int coarse_segments(int64_t nq, int nlist, int d) {
 
 void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                              int nprobe, uint64_t* cand, float* out_dis, int64_t* out_list, hipStream_t s, bool ip,
-                             const ListPlan* plan, const int64_t* list_off, int lo, int hi, const float* cent,
-                             float* xn_buf) {
+                             const ListPlan* plan, const int64_t* list_off, int lo, int hi, const float* cent) {
   if (nq <= 0) return;
   const int nseg = coarse_segments(nq, nlist, d);
   const int tiles = (nlist + GC - 1) / GC;
   const int seg = (tiles + nseg - 1) / nseg * GC;
-  if (xn_buf && segmented_tiled(nq, d)) {
-    if (!ip) launch_row_norms(x, nq, d, xn_buf, s);
-    hipLaunchKernelGGL(k_coarse_segtop_tiled, dim3((unsigned)(nblocks(nq, TQ) * (unsigned)nseg)), dim3(256), 0, s, x,
-                       xn_buf, nq, d, centT, (nlist + 3) & ~3, cn, nlist, ip ? 1 : 0, seg, nseg, nprobe, cand);
-  } else {
   const int dk = (d + 63) & ~63;
   const size_t smem = sizeof(float) * ((size_t)dk * GQ + GQ + GQ * 8 + GQ * GC) + sizeof(uint64_t) * GQ * kSegQ;
   if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device
@@ -4164,7 +3496,6 @@ void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* cen
   const unsigned grid = (unsigned)(nblocks(nq, GQ) * (unsigned)nseg);
   hipLaunchKernelGGL(k_coarse_segtop, dim3(grid), dim3(256), smem, s, x, nq, d, centT, (nlist + 3) & ~3, cn, nlist,
                      ip ? 1 : 0, seg, nseg, nprobe, cand);
-  }
   CoarsePlan cp;
   if (plan) {
     cp.pl = *plan;
@@ -4304,13 +3635,6 @@ int scan_lists_grid(int M, int k) {
   return std::max(8, (per_cu * cus + 7) / 8 * 8);
 }
 
-// the pipelined scan (k_scan_pipe) serves k <= 16 at M <= 16 with fused planning;
-// (off by default: one item per CU at a time measured slower than two
-// k_scan_lists workgroups per CU; -DSCAN_PIPE=1 builds it)
-#ifndef SCAN_PIPE
-#define SCAN_PIPE 0
-#endif
-
 int device_cus() {
   static int cus = 0;
   if (!cus) {
@@ -4321,31 +3645,14 @@ int device_cus() {
   return cus;
 }
 
-#ifdef WZ_BISECT  // experiment: which launches of a search run from a forcezero build (profiles/build_wz_bisect.sh)
-int g_launch_parts = 3;  // bit 0: the list scan, bit 1: the merges
-void set_launch_parts(int p) { g_launch_parts = p; }
-#endif
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
   // code chunks held in registers per item (32 VGPRs), even; r02 A/B at C2 M = 16:
   // 6 -> 111.8 us, 8 -> 114.3, 4 -> 113.9
-#ifndef JB_WIDE
-#define JB_WIDE 4  // code chunks in registers per item at M > 32 (r04 A/B vs 2: C3 scan 643 -> 624 us, C4 214 -> 210 us)
-#endif
-  constexpr int JB = M <= 16 ? 6 : M <= 32 ? 4 : JB_WIDE;
+  // (M > 32: 4 chunks, r04 A/B vs 2: C3 scan 643 -> 624 us, C4 214 -> 210 us)
+  constexpr int JB = M <= 16 ? 6 : 4;
   if (ev) (void)hipEventRecord(ev[0], s);
-#ifdef WZ_BISECT
-  if (g_launch_parts & 1) {
-#endif
-  if constexpr (G == 4 && R == 1 && M <= 16 && SCAN_PIPE) {
-    if (a.k <= 16 && pl.fused) {  // one workgroup per CU
-      hipLaunchKernelGGL((k_scan_pipe<M, 2>), dim3((unsigned)device_cus()), dim3(kPipeT), 0, s, a, pl);
-      if (ev) (void)hipEventRecord(ev[1], s);
-      hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
-      return;
-    }
-  }
   if constexpr (G == 4 && R == 1) {
     if (a.k <= 16) {  // r03 A/B at C2: 115.1 vs 125.7 us
       hipLaunchKernelGGL((k_scan_lists<M, G, R, JB, true>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
@@ -4355,13 +3662,9 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   } else {
     hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
   }
-#ifdef WZ_BISECT
-  }
-  if (!(g_launch_parts & 2)) return;
-#endif
   if (ev) (void)hipEventRecord(ev[1], s);
   if (R >= 2 && a.nprobe <= 64) {
-    if (MERGE_RADIX && 4 * a.nprobe * pl.ks <= kRadixU * 256)  // every key of a query in one workgroup's registers
+    if (4 * a.nprobe * pl.ks <= kRadixU * 256)  // every key of a query in one workgroup's registers
       hipLaunchKernelGGL(k_merge_radix, dim3((unsigned)a.nq), dim3(256), 0, s, a, pl);
     else
       hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
@@ -4400,7 +3703,7 @@ void launch_merge_topk(int S, int64_t n, int k, const float* Din, const int64_t*
 
 }  // namespace chivf
 
-#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS) || defined(DIAG_PSTAMPS)
+#if defined(DIAG_STAMPS) || defined(DIAG_CSTAMPS)
 extern "C" int ivfpq_diag_stamps(void* out, size_t bytes) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(chivf::g_diag), bytes) != hipSuccess) return -1;
   static uint64_t zeros[chivf::kDiagWG * chivf::kDiagItems * chivf::kDiagSlots];

@@ -41,6 +41,10 @@ SIGNATURES = {
     "ivfpq_get_inflight": (ctypes.c_int, [c_handle]),
     "ivfpq_overlap_built": (ctypes.c_int, []),
     "ivfpq_get_error_count": (ctypes.c_int, [c_handle, c_i64p]),
+    "ivfpq_get_repair_stats": (ctypes.c_int, [c_handle, c_i64p, c_i64p]),
+    "ivfpq_get_repair_log": (ctypes.c_int, [c_handle, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_int)]),
+    "ivfpq_set_fault_injection": (ctypes.c_int, [c_handle, ctypes.c_int]),
     "ivfpq_add_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
     "ivfpq_add_preencoded": (ctypes.c_int, [c_handle, ctypes.c_int64, c_i64p, c_u8p, c_i64p]),

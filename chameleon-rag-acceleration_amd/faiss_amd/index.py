@@ -222,8 +222,8 @@ class _InvertedLists:
 
 
 def overlap_built():
-    """True when the loaded library has the experimental batches-in-flight overlap
-    (ivfpq_overlap_built; built with -DIVFPQ_OVERLAP=1)."""
+    """True: the batches-in-flight overlap is available (ivfpq_overlap_built; kept
+    for callers of the r04 interface, where it was a build option)."""
     return bool(_lib.load().ivfpq_overlap_built())
 
 class IndexIVFPQ:
@@ -510,6 +510,32 @@ class IndexIVFPQ:
         out = ctypes.c_int64(0)
         _lib.check(_lib.load().ivfpq_get_error_count(self._h, ctypes.byref(out)))
         return out.value
+
+    def repair_stats(self):
+        """(stale_reads, repairs) since creation: (query, merge launch) pairs that read a
+        partial-list entry this batch's scan did not leave there, and the probes the merge
+        rescanned because of one (ivfpq_get_repair_stats).  Waits for in-flight searches."""
+        st, rp = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.check(_lib.load().ivfpq_get_repair_stats(self._h, ctypes.byref(st), ctypes.byref(rp)))
+        return st.value, rp.value
+
+    def repair_log(self, max_events=192):
+        """The first stale-entry events as dicts (ivfpq_get_repair_log)."""
+        buf = (ctypes.c_uint32 * (8 * max_events))()
+        n = ctypes.c_int(0)
+        _lib.check(_lib.load().ivfpq_get_repair_log(self._h, buf, int(max_events), ctypes.byref(n)))
+        out = []
+        for e in range(n.value):
+            w = buf[8 * e:8 * e + 8]
+            out.append({"site": w[0] & 0xFF, "reader_xcd": (w[0] >> 8) & 0xF, "query": w[1], "list": w[2] & 0xFFFF,
+                         "rank": w[2] >> 16, "expected_tag": w[3], "found_tag": w[4] & 0x0FFFFFFF,
+                         "writer_xcd": w[4] >> 28, "found_key_bits": w[5], "epoch": w[6], "reread": w[7]})
+        return out
+
+    def set_fault_injection(self, every):
+        """Test hook: later searches skip the partial-list stores of slots with
+        slot % every == 1 (0 = off); results must stay exact (repairs)."""
+        _lib.check(_lib.load().ivfpq_set_fault_injection(self._h, int(every)))
 
     def search_device(self, x, k, D=None, I=None, stream=None):
         """Search with inputs resident in HBM.  ``x`` is a torch float32 CUDA

@@ -24,7 +24,13 @@
  * environment when the handle is created) searches on up to three streams
  * overlap, each in the per-stream workspace it last used; a fourth stream takes
  * over the least recently used workspace after waiting on the host for its
- * last search.  Results are identical in both modes.
+ * last search.
+ * Results under concurrent GPU work: every per-wave partial list the merge reads
+ * is a set of tagged records (batch epoch + slot); an entry this batch's scan did
+ * not leave there (measured in r04: ~1e-4 of batches beside another kernel on the
+ * GPU) is never used -- its probe is rescanned on the device
+ * by the merge, so results stay identical to the oracle's.  The detections and
+ * rescans are counted (ivfpq_get_repair_stats).
  */
 #ifndef CHAMELEON_IVFPQ_H
 #define CHAMELEON_IVFPQ_H
@@ -132,14 +138,11 @@ int ivfpq_search_preassigned_tables_device(ivfpq_index* h, int64_t n, const floa
 
 /* Batches in flight (see "Stream ordering" above): 1 = device searches on different
  * streams overlap, 0 = each waits for the others (default, unless IVFPQ_INFLIGHT=1).
- * Experimental, not built by default (ivfpq_overlap_built): ~1e-4 of overlapped
- * batches differ from the oracle.
  * Waits for the handle's in-flight searches before switching.  Reference: the query
  * blocks streamed through one GPU index, bench_gpu_1bn.py:788-806. */
 int ivfpq_set_inflight(ivfpq_index* h, int on);
 int ivfpq_get_inflight(const ivfpq_index* h);
-/* 1 when the library was built with the overlap (-DIVFPQ_OVERLAP=1); otherwise
- * ivfpq_set_inflight(h, 1) fails with a message and searches are always ordered. */
+/* 1: the overlap is available (kept for callers of the r04 interface). */
 int ivfpq_overlap_built(void);
 
 /* Index checks of the merge kernels: code positions read back from partial lists
@@ -148,6 +151,23 @@ int ivfpq_overlap_built(void);
  * handle was created, over all its workspaces, after waiting for in-flight
  * searches.  0 on a correct run; the tests assert it. */
 int ivfpq_get_error_count(ivfpq_index* h, int64_t* out);
+
+/* Stale partial lists (see "Results under concurrent GPU work" above): *stale_reads =
+ * (query, merge launch) pairs that read an entry whose tag was not this batch's,
+ * *repairs = probes the merge rescanned because of one; totals since the handle was
+ * created, over all workspaces, after waiting for in-flight searches. */
+int ivfpq_get_repair_stats(ivfpq_index* h, int64_t* stale_reads, int64_t* repairs);
+/* The first stale-entry events (at most 64 per workspace), 8 uint32 each: merge site
+ * (1 fast path, 2 full merge) | reader XCD << 8, query, list j | rank << 16, expected
+ * tag, found tag (writer XCD in bits 28-31), found key bits, batch epoch, and the
+ * number of system-scope re-reads until the tag was fresh (0xFFFFFFFF = never within
+ * 2000; fast path: 1 = fresh at once, 0 = not).  *n_events = events copied to out
+ * (out holds max_events x 8 words). */
+int ivfpq_get_repair_log(ivfpq_index* h, uint32_t* out, int max_events, int* n_events);
+/* Test hook for the repair path: every > 0 makes the list scan of later searches skip
+ * the stores of the partial lists whose slot (pair * 4 + wave) % every == 1, as if
+ * they were lost; 0 (default) turns it off.  Results must stay exact. */
+int ivfpq_set_fault_injection(ivfpq_index* h, int every);
 
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing

@@ -7,8 +7,10 @@ searched alone.  Per (k, streams, round): mismatching batches / rows, whether
 the bad rows hold sentinel labels or non-finite keys, and the merge kernels'
 index-check count.  Round 0 of each configuration is the first use of the
 workspaces at that k (buffers grow there); later rounds reuse them.
-Prints one JSON line per configuration.  The overlap cases need a library built with
--DIVFPQ_OVERLAP=1 (profiles/build_variants.sh ov:"-DIVFPQ_OVERLAP=1", then IVFPQ_LIB=...)."""
+Prints one JSON line per configuration, with the library's stale-entry counters
+(repair_stats, cumulative over the configurations) and its first logged events
+(repair_log).  r05: partial lists are tagged records; a stale entry is detected and
+its probe rescanned by the merge, so "bad_batches" must now be 0."""
 import json
 import os
 import sys
@@ -23,7 +25,7 @@ def main():
     import torch
 
     import faiss_amd as faiss
-    from faiss_amd import datasets
+    from faiss_amd import _lib, datasets
 
     configs = [(100, 3), (100, 2), (10, 3), (100, 4)]
     if len(sys.argv) > 1:
@@ -105,7 +107,18 @@ def main():
                                   "D": D[r, diff[:6]].tolist(), "D_ref": Dr[r, diff[:6]].tolist()}
             per_round.append({"bad_batches": bad_b, "bad_rows": bad_rows, "sentinels": sent, "nonfinite": nonfin,
                               "err": ix.error_count() - e0})
+        st, rp = ix.repair_stats()
+        dbg = None
+        lib = _lib.load()
+        if hasattr(lib, "ivfpq_dbg_read"):  # debug variant (profiles/race_variants.py dbg)
+            import ctypes
+            buf = (ctypes.c_uint32 * (1 + 64 * 48))()
+            lib.ivfpq_dbg_read(buf, 1)
+            n = min(buf[0], 64)
+            dbg = {"count": buf[0], "events": [list(buf[1 + 48 * e:1 + 48 * e + 31]) for e in range(min(n, 12))]}
         print(json.dumps({"k": k, "streams": nst, "hog": hog, "mix": mix, "rounds": rounds,
+                          "inflight": nst > 1 and os.environ.get("RACE_INFLIGHT", "1") != "0",
+                          "stale_reads_total": st, "repairs_total": rp, "log": ix.repair_log(64), "dbg": dbg,
                           "bad_batches": sum(r["bad_batches"] for r in per_round),
                           "bad_rounds": [dict(r, round=i) for i, r in enumerate(per_round) if r["bad_batches"] or r["err"]], "first": detail,
                           "s": round(time.time() - t0, 1)}), flush=True)
