@@ -1405,6 +1405,27 @@ int ivfpq_get_repair_log(ivfpq_index* h, uint32_t* out, int max_events, int* n_e
   });
 }
 
+int ivfpq_debug_workspace(ivfpq_index* h, int ws, int what, void* dst, int64_t cap, int64_t* bytes) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(ws >= 0 && ws < ivfpq_index::kSlots && bytes != nullptr, "bad workspace index");
+    h->quiesce();
+    auto& w = h->work[ws];
+    if (what >= 7) {  // host words: 7 the epoch of the last batch planned there, 8 the stream it ran on
+      const uint64_t v = what == 7 ? (uint64_t)w.epoch : (uint64_t)(uintptr_t)w.done_stream;
+      *bytes = 8;
+      if (dst && cap >= 8) std::memcpy(dst, &v, 8);
+      return;
+    }
+    const DevBuf* b = what == 0 ? &w.p_part : what == 1 ? &w.p_N : what == 2 ? &w.p_qmask : what == 3 ? &w.p_tau
+                    : what == 4 ? &w.p_hdr : what == 5 ? &w.w_lists : &w.w_dis0;
+    *bytes = (int64_t)b->bytes;
+    if (dst && b->p) HIPCHECK(hipMemcpy(dst, b->p, std::min<size_t>(b->bytes, (size_t)cap), hipMemcpyDeviceToHost));
+  });
+}
+
 int ivfpq_set_fault_injection(ivfpq_index* h, int every) {
   return guarded([&] {
     check_handle(h);

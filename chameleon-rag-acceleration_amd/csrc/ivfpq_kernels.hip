@@ -1843,14 +1843,22 @@ __device__ __forceinline__ int2 fused_plan_prefix(const ListPlan& pl, int nloc, 
   return make_int2(ta, tb);
 }
 
-// word (lane & 15) of item e's record (layout of write_item), as RAW loads that
-// nothing here consumes (no wait: the record is in flight during the current
-// item's scan); unpack derives the fields: word 1 = the list's pair count
-// (count = min(G, min(c, cap) - t G), t in word 14), words 2 / 3 = the low
-// words of off[l + 1] / off[l] (n = w2 - w3), word 4 = off[l]'s high word.
-__device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& pl, int nloc, int e, int n0,
-                                            const uint16_t* ex0, const uint16_t* ex1, const uint16_t* ord, int G,
-                                            int lane) {
+// Item e's record, fetched ahead: lane w (< 16) issues ONE unconditional load of
+// record word w -- no divergent branches, so no register receives loads under
+// different exec masks -- whose value nothing consumes until unpack (the load stays
+// in flight during the current item's scan).  Fused planning: word 1 = the list's
+// pair count (count = min(G, min(c, cap) - t G)), words 2 / 3 = the low words of
+// off[l + 1] / off[l] (n = w2 - w3), word 4 = off[l]'s high word, words 5..8 / 9..12
+// = the bucket's pair ids / dis0 bits; the list, kind and t are wave-uniform and
+// kept in scalars (the other lanes load word 1 again).  Non-fused: the 16 words of
+// pl.recs (write_item's layout).
+struct Rec {
+  int raw;  // this lane's loaded word (in flight)
+  int l, kind, t;
+};
+__device__ __forceinline__ Rec fused_record(const ScanArgs& a, const ListPlan& pl, int nloc, int e, int n0,
+                                           const uint16_t* ex0, const uint16_t* ex1, const uint16_t* ord, int G,
+                                           int lane) {
   const int kind = e < n0 ? 0 : 1;
   const int ek = kind ? e - n0 : e;
   const uint16_t* ex = kind ? ex1 : ex0;
@@ -1860,23 +1868,24 @@ __device__ __forceinline__ int fused_record(const ScanArgs& a, const ListPlan& p
   const int j0 = 16 * (63 - __builtin_clzll(m1));
   const uint64_t m2 = __builtin_amdgcn_ballot_w64(lane < 16 && j0 + lane < nloc && (int)ex[j0 + lane] <= ek);
   const int j = j0 + 63 - __builtin_clzll(m2);
-  const int jl = ord[j];
-  const int t = ek - (int)ex[j];
+  const int jl = __builtin_amdgcn_readfirstlane((int)ord[j]);
+  const int t = ek - __builtin_amdgcn_readfirstlane((int)ex[j]);
   const int64_t l = a.list_lo + jl;
   const int* off32 = reinterpret_cast<const int*>(a.list_off);
   const int* bk32 = reinterpret_cast<const int*>(pl.bucket);
   const int w = lane & 15;
-  int v = 0;
-  if (w == 0) v = (int)l;
-  else if (w == 1) v = pl.cnt[kind * nloc + jl];
-  else if (w == 2) v = off32[2 * (l + 1)];
-  else if (w == 3) v = off32[2 * l];
-  else if (w == 4) v = off32[2 * l + 1];
-  else if (w <= 12)  // slots past the item's count hold other pairs: never used
-    v = bk32[2 * (((int64_t)jl * 2 + kind) * pl.cap + min(t * G + ((w - 5) & 3), pl.cap - 1)) + (w <= 8 ? 0 : 1)];
-  else if (w == 13) v = kind;
-  else if (w == 14) v = t;
-  return v;
+  const int64_t slot = ((int64_t)jl * 2 + kind) * pl.cap + min(t * G + ((w - 5) & 3), pl.cap - 1);
+  const int* src = w == 2 ? off32 + 2 * (l + 1)
+                 : w == 3 ? off32 + 2 * l
+                 : w == 4 ? off32 + 2 * l + 1
+                 : (w >= 5 && w <= 12) ? bk32 + 2 * slot + (w <= 8 ? 0 : 1)
+                 : pl.cnt + kind * nloc + jl;  // word 1 (and the unused lanes)
+  Rec r;
+  r.raw = *src;
+  r.l = (int)l;
+  r.kind = kind;
+  r.t = t;
+  return r;
 }
 
 // A wave's sorted partial list of one pair into slot `slot` = pair * 4 + wave, as
@@ -1945,23 +1954,30 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   // flight while the previous item is scanned), unpacked with readlane.  Fused
   // planning derives the words from the LDS prefix, the counts and the buckets.
   Item<G> it;
-  auto fetch_rec = [&](int idx) __attribute__((always_inline)) -> int {
-    if (!pl.fused) return pl.recs[(int64_t)idx * 16 + (lane & 15)];
+  auto fetch_rec = [&](int idx) __attribute__((always_inline)) -> Rec {
+    if (!pl.fused) {
+      Rec r;
+      r.raw = pl.recs[(int64_t)idx * 16 + (lane & 15)];
+      r.l = r.kind = r.t = 0;  // (words 0, 13 of the raw record)
+      return r;
+    }
     return fused_record(a, pl, nloc, idx, n_items0, s_ex[0], s_ex[1], s_ord, G, lane);
   };
-  auto unpack = [&](int rv) __attribute__((always_inline)) {
-    it.l = __builtin_amdgcn_readlane(rv, 0);
+  auto unpack = [&](const Rec& rc) __attribute__((always_inline)) {
+    const int rv = rc.raw;
     if (pl.fused) {  // raw words (fused_record)
-      const int t = __builtin_amdgcn_readlane(rv, 14);
-      it.cnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - t * G);
+      it.l = rc.l;
+      it.kind = rc.kind;
+      it.cnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - rc.t * G);
       it.n = __builtin_amdgcn_readlane(rv, 2) - __builtin_amdgcn_readlane(rv, 3);
     } else {
+      it.l = __builtin_amdgcn_readlane(rv, 0);
+      it.kind = __builtin_amdgcn_readlane(rv, 13);
       it.cnt = __builtin_amdgcn_readlane(rv, 1);
       it.n = __builtin_amdgcn_readlane(rv, 2);
     }
     it.beg = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
                        (uint32_t)__builtin_amdgcn_readlane(rv, 3));
-    it.kind = __builtin_amdgcn_readlane(rv, 13);
 #pragma unroll
     for (int g = 0; g < G; g++) {
       it.pair[g] = __builtin_amdgcn_readlane(rv, 5 + g);
@@ -2075,7 +2091,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
     __syncthreads();  // (B) the LUT, s_next and s_wb are visible
     DIAG(1, __builtin_amdgcn_s_memtime());
     const int nxt = s_next;
-    const int nrec = fetch_rec(nxt >= 0 ? nxt : cur);  // the next record, in flight during the scan
+    const Rec nrec = fetch_rec(nxt >= 0 ? nxt : cur);  // the next record, in flight during the scan
     int qix[G];  // the pairs' queries
     float bound[G];
     bool loose = false;  // some query of the item has no bound yet

@@ -45,6 +45,8 @@ SIGNATURES = {
     "ivfpq_get_repair_log": (ctypes.c_int, [c_handle, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_int)]),
     "ivfpq_set_fault_injection": (ctypes.c_int, [c_handle, ctypes.c_int]),
+    "ivfpq_debug_workspace": (ctypes.c_int, [c_handle, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                             c_i64p]),
     "ivfpq_add_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
     "ivfpq_add_preencoded": (ctypes.c_int, [c_handle, ctypes.c_int64, c_i64p, c_u8p, c_i64p]),

@@ -168,6 +168,11 @@ int ivfpq_get_repair_log(ivfpq_index* h, uint32_t* out, int max_events, int* n_e
  * the stores of the partial lists whose slot (pair * 4 + wave) % every == 1, as if
  * they were lost; 0 (default) turns it off.  Results must stay exact. */
 int ivfpq_set_fault_injection(ivfpq_index* h, int every);
+/* Diagnostics: copy (up to cap bytes of) one per-batch buffer of workspace ws (0..2) as the
+ * last search on it left it -- what: 0 partial-list records, 1 partial-list counts, 2 probe
+ * masks, 3 tau words, 4 header words, 5 coarse lists, 6 coarse dis0; 7 / 8: the epoch of the
+ * last batch planned there / the stream it ran on (8 bytes each); *bytes = its size. */
+int ivfpq_debug_workspace(ivfpq_index* h, int ws, int what, void* dst, int64_t cap, int64_t* bytes);
 
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing

@@ -54,6 +54,12 @@ def main():
             torch.cuda.synchronize()
             ref.append((D.cpu().numpy(), I.cpu().numpy()))
         refs[k] = ref
+    # coarse references (modes 3 and 4): the probes of every batch, searched alone
+    cref = []
+    for b in range(nb):
+        Dq, Iq = ix.coarse_device(xd[b])
+        torch.cuda.synchronize()
+        cref.append((Dq.clone(), Iq.clone()))
     big = np.iinfo(np.int64).max
     hog_a = torch.empty(1 << 27, device="cuda")
     hog_b = torch.empty_like(hog_a)
@@ -62,6 +68,8 @@ def main():
         k, nst = cfg[0], cfg[1]
         hog = len(cfg) > 2 and cfg[2] == 1
         mix = len(cfg) > 2 and cfg[2] == 2
+        coarse_only = len(cfg) > 2 and cfg[2] == 3  # mode 3: coarse_device only, vs its reference
+        pre_only = len(cfg) > 2 and cfg[2] == 4     # mode 4: search_preassigned_device with the reference probes
         t0 = time.time()
         streams = [torch.cuda.Stream() for _ in range(nst)]
         per_round = []
@@ -83,7 +91,16 @@ def main():
                         with torch.cuda.stream(st):
                             Dq, Iq = ix.coarse_device(xd[b], stream=st.cuda_stream)
                             ix.search_preassigned_device(xd[b], k, Iq, Dq, stream=st.cuda_stream)
-                    ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=st.cuda_stream)
+                    if coarse_only:
+                        with torch.cuda.stream(st):
+                            cq = ix.coarse_device(xd[b], stream=st.cuda_stream)
+                        outs[b] = (cq[0], cq[1])
+                    elif pre_only:
+                        with torch.cuda.stream(st):
+                            ix.search_preassigned_device(xd[b], k, cref[b][1], cref[b][0], outs[b][0], outs[b][1],
+                                                         stream=st.cuda_stream)
+                    else:
+                        ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=st.cuda_stream)
                 torch.cuda.synchronize()
             finally:
                 ix.inflight = False
@@ -92,6 +109,8 @@ def main():
                 D = outs[b][0].cpu().numpy()
                 I = outs[b][1].cpu().numpy()
                 Dr, Ir = refs[k][b]
+                if coarse_only:
+                    Dr, Ir = cref[b][0].cpu().numpy(), cref[b][1].cpu().numpy()
                 rows = np.nonzero((I != Ir).any(axis=1) | (D != Dr).any(axis=1))[0]
                 if len(rows):
                     bad_b += 1
@@ -117,6 +136,7 @@ def main():
             n = min(buf[0], 64)
             dbg = {"count": buf[0], "events": [list(buf[1 + 48 * e:1 + 48 * e + 31]) for e in range(min(n, 12))]}
         print(json.dumps({"k": k, "streams": nst, "hog": hog, "mix": mix, "rounds": rounds,
+                          "mode": "coarse" if coarse_only else "preassigned" if pre_only else "search",
                           "inflight": nst > 1 and os.environ.get("RACE_INFLIGHT", "1") != "0",
                           "stale_reads_total": st, "repairs_total": rp, "log": ix.repair_log(64), "dbg": dbg,
                           "bad_batches": sum(r["bad_batches"] for r in per_round),

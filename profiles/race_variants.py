@@ -212,6 +212,85 @@ def noswap(s):  # the lane ^ 16 / ^ 32 exchanges by ds_bpermute instead of v_per
   }""", """  else return __shfl_xor(v, J, 64);""")
 
 
+def notau(s):  # no cross-workgroup bound: tau_q never read (every item starts unbounded) nor lowered
+    s = sub(s, "  return (uint32_t)(v >> 32) == ~pl.epoch ? (int)((uint32_t)v ^ 0x80000000u) : f2ord(kInf);",
+            "  (void)v;\n  return f2ord(kInf);")
+    s = sub(s, "  atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);",
+            "  (void)w;")
+    return s
+
+
+def nowb(s):  # no cross-wave bound inside an item (s_wb never read)
+    return sub(s, "        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));",
+               "        (void)s_wb;")
+
+
+TLOG_HELPERS = r"""
+namespace chivf {
+__device__ uint32_t* g_tlog;
+__device__ uint32_t g_tlog_cap;
+__device__ uint32_t g_tlog_n;
+}
+extern "C" int ivfpq_dbg_set_tlog(void* ptr, uint32_t cap) {
+  uint32_t zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(chivf::g_tlog), &ptr, sizeof(ptr)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(chivf::g_tlog_cap), &cap, sizeof(cap)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(chivf::g_tlog_n), &zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+extern "C" int ivfpq_dbg_tlog_count(uint32_t* n) {
+  return hipMemcpyFromSymbol(n, HIP_SYMBOL(chivf::g_tlog_n), sizeof(uint32_t)) == hipSuccess ? 0 : -1;
+}
+"""
+
+
+def taulog(s):
+    # every tau lowering logged: (tauq address low word, epoch, query, value, site, pair, list, block | wave << 16)
+    s = sub(s, "// a code position read back from a partial list, checked against the image",
+            """__device__ __forceinline__ void tlog(const ListPlan& pl, const float* outD, int64_t q, int o, int site, int pair, int l) {
+  if (!g_tlog) return;
+  const uint32_t e = atomicAdd(&g_tlog_n, 1u);
+  if (e >= g_tlog_cap) return;
+  uint4* r = reinterpret_cast<uint4*>(g_tlog) + 2 * (size_t)e;
+  r[0] = make_uint4((uint32_t)(uintptr_t)outD, pl.epoch, (uint32_t)q, (uint32_t)o);
+  r[1] = make_uint4((uint32_t)site, (uint32_t)pair, (uint32_t)l, blockIdx.x | ((threadIdx.x >> 6) << 16));
+}
+// a code position read back from a partial list, checked against the image""")
+    s = sub(s, """          atomicMin(&s_wb[g], f2ord(kc_key(tp)));
+          tau_lower(pl, qix[g], f2ord(kc_key(tp)));""", """          atomicMin(&s_wb[g], f2ord(kc_key(tp)));
+          tau_lower(pl, qix[g], f2ord(kc_key(tp)));
+          tlog(pl, a.outD, qix[g], f2ord(kc_key(tp)), ROWK ? 11 : 12, it.pair[g], it.l);""")
+    s = sub(s, """              atomicMin(&s_wb[g], f2ord(T));
+              tau_lower(pl, qix[g], f2ord(T));""", """              atomicMin(&s_wb[g], f2ord(T));
+              tau_lower(pl, qix[g], f2ord(T));
+              tlog(pl, a.outD, qix[g], f2ord(T), 2, it.pair[g], it.l);""")
+    s = sub(s, """              atomicMin(&s_wb[g], T);
+              tau_lower(pl, qix[g], T);""", """              atomicMin(&s_wb[g], T);
+              tau_lower(pl, qix[g], T);
+              tlog(pl, a.outD, qix[g], T, 3, it.pair[g], it.l);""")
+    return s
+
+
+def tau_nop_after(s):  # 16 wait states right after every tau_q atomicMin (its data registers left alone that long)
+    return sub(s, "  atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);",
+               "  atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);\n"
+               "  asm volatile(\"s_nop 7\\n\\ts_nop 7\" ::: \"memory\");")
+
+
+def tau_nop_before(s):  # the same 16 wait states right before it (control: same perturbation, no protection after)
+    return sub(s, "  atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);",
+               "  asm volatile(\"s_nop 7\\n\\ts_nop 7\" ::: \"memory\");\n"
+               "  atomicMin(reinterpret_cast<unsigned long long*>(pl.tauq + q), (unsigned long long)w);")
+
+
+def nofast(s):  # keep tau, but never take the packed-prefix (fast) admission: per-chunk admission always
+    return sub(s, "      } else if (!loose) {", "      } else if (!loose && a.k < 0) {")
+
+
+def noloose(s):  # keep tau, but never derive bounds from the super-batch lane minima (loose path off)
+    return sub(s, "        if (loose) {\n#pragma unroll\n          for (int g = 0; g < G; g++) {\n            if (bound[g] != kInf) continue;  // wave-uniform\n            float mn = kInf;",
+               "        if (loose && a.k < 0) {\n#pragma unroll\n          for (int g = 0; g < G; g++) {\n            if (bound[g] != kInf) continue;  // wave-uniform\n            float mn = kInf;")
+
+
 VARIANTS = {
     "base": lambda s: s,
     "wt_part": wt_part,
@@ -220,6 +299,13 @@ VARIANTS = {
     "acq_start": lambda s: kernel_start(s, "{ if (threadIdx.x == 0) { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"agent\"); "
                                            "asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\"); } __syncthreads(); }"),
     "dbg": dbg,
+    "nofast": nofast,
+    "noloose": noloose,
+    "tau_nop_after": tau_nop_after,
+    "tau_nop_before": tau_nop_before,
+    "taulog": taulog,
+    "notau": notau,
+    "nowb": nowb,
     "w_unpack": w_unpack,
     "w_fetch": w_fetch,
     "p_merge": p_merge,
@@ -235,7 +321,7 @@ def build(name):
     src = VARIANTS[name](src)
     if name != "base":
         i = src.index("namespace chivf {")
-        src = src[:i] + HELPERS + (DBG_HELPERS if name == "dbg" else "") + src[i:]
+        src = src[:i] + HELPERS + (DBG_HELPERS if name == "dbg" else "") + (TLOG_HELPERS if name == "taulog" else "") + src[i:]
     out = os.path.join(R, "chameleon-rag-acceleration_amd", "lib", "var", name)
     os.makedirs(out, exist_ok=True)
     kp = os.path.join(out, "ivfpq_kernels.hip")
