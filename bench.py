@@ -91,12 +91,11 @@ def parse():
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
-    p.add_argument("--inflight", type=int, default=1,
-                   help="batches in flight on that many HIP streams (step s on stream s %% N; > 1 turns the "
-                        "index's batches-in-flight mode on so that consecutive batches overlap, DESIGN.md "
-                        "section 4 -- experimental, needs a -DIVFPQ_OVERLAP=1 build: ~1e-4 of overlapped batches "
-                        "differ from the oracle); "
-                        "1 = one batch at a time on one stream (the parity-clean path, default)")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="batches in flight on that many HIP streams (step s on stream s %% N, each with its own "
+                        "workspace and, sharded, its own communicator; > 1 turns the index's batches-in-flight "
+                        "mode on so that consecutive batches overlap, DESIGN.md section 4); 1 = one batch at a "
+                        "time on one stream (also measured beside the value as ms_per_step_serial)")
     return p.parse_args()
 
 
@@ -154,10 +153,10 @@ def main():
     xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
     k = args.k
     inflight = max(1, args.inflight)
-    if inflight > 1 and not faiss.overlap_built():
-        raise SystemExit("--inflight > 1 needs the experimental overlap, which this library was built without "
-                         "(-DIVFPQ_OVERLAP=1; DESIGN.md section 4)")
     ix.inflight = inflight > 1
+    # sharded: one communicator per in-flight stream, so that the collectives of two
+    # batches in flight never share one (every rank creates them in the same order)
+    groups = [dist.new_group(list(range(world))) for _ in range(inflight)] if shard else None
     streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
     Dbufs = [torch.empty((Bg, k), dtype=torch.float32, device=dev) for _ in range(inflight)]
     Ibufs = [torch.empty((Bg, k), dtype=torch.int64, device=dev) for _ in range(inflight)]
@@ -184,9 +183,9 @@ def main():
                 sides[j].wait_stream(streams[j])
                 tok = ix.precompute_tables_device(xg, stream=sides[j].cuda_stream)
                 Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
-                Dq, Iq = all_gather_probes(Dq_s, Iq_s, world)
+                Dq, Iq = all_gather_probes(Dq_s, Iq_s, world, groups[j])
                 Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j], tables=tok)
-                Ds, Is = exchange_partials(Dp, Ip, world)
+                Ds, Is = exchange_partials(Dp, Ip, world, groups[j])
                 merged[b] = faiss.merge_topk_device(Ds, Is)
         else:  # stream j of the in-flight set, with its own output buffers
             ix.search_device(xq_dev[b], k, Dbufs[j], Ibufs[j], stream=streams[j].cuda_stream)
@@ -246,40 +245,31 @@ def main():
         I100 = torch.empty((Bg, 100), dtype=torch.int64, device=dev)
         D100 = [D100] + [torch.empty_like(D100) for _ in range(inflight - 1)]
         I100 = [I100] + [torch.empty_like(I100) for _ in range(inflight - 1)]
-        ix.search_device(xq_dev[0], 100, D100[0], I100[0])
+        for j in range(inflight):
+            ix.search_device(xq_dev[j % args.nbatches], 100, D100[j], I100[j], stream=streams[j].cuda_stream)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for s in range(n_ex):  # one stream: the library orders k > 64 searches anyway
-            ix.search_device(xq_dev[s % args.nbatches], 100, D100[0], I100[0], stream=streams[0].cuda_stream)
+        for s in range(n_ex):  # k = 100 with the same batches in flight as the value
+            j = s % inflight
+            ix.search_device(xq_dev[s % args.nbatches], 100, D100[j], I100[j], stream=streams[j].cuda_stream)
         torch.cuda.synchronize()
         extra["k100_queries_per_s"] = n_ex * Bg / (time.perf_counter() - t0)
+        ix.inflight = False
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(n_ex):
+            ix.search_device(xq_dev[s % args.nbatches], 100, D100[0], I100[0], stream=streams[0].cuda_stream)
+        torch.cuda.synchronize()
+        extra["k100_queries_per_s_serial"] = n_ex * Bg / (time.perf_counter() - t0)
+        ix.inflight = inflight > 1
         xq_host = [np.ascontiguousarray(xq[b * Bg:(b + 1) * Bg]) for b in range(args.nbatches)]
         ix.search(xq_host[0], k)
         t0 = time.perf_counter()
         for s in range(n_ex):
             ix.search(xq_host[s % args.nbatches], k)
         extra["host_search_queries_per_s"] = n_ex * Bg / (time.perf_counter() - t0)
-        if inflight == 1 and faiss.overlap_built():  # experimental overlap (-DIVFPQ_OVERLAP=1 builds), beside the value only
-            st2 = [torch.cuda.Stream(dev) for _ in range(2)]
-            D2 = [torch.empty_like(Dbuf) for _ in range(2)]
-            I2 = [torch.empty_like(Ibuf) for _ in range(2)]
-            ix.inflight = True
-            try:
-                for j in range(2):
-                    ix.search_device(xq_dev[j % args.nbatches], k, D2[j], I2[j], stream=st2[j].cuda_stream)
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for s in range(args.steps):
-                    ix.search_device(xq_dev[s % args.nbatches], k, D2[s % 2], I2[s % 2], stream=st2[s % 2].cuda_stream)
-                torch.cuda.synchronize()
-                extra["overlap2_queries_per_s_experimental"] = args.steps * Bg / (time.perf_counter() - t0)
-            finally:
-                ix.inflight = False
-        extra["note"] = (f"{n_ex} batches each; k100 = search_device with k=100 (one stream: k > 64 searches "
-                         f"are not overlapped); overlap2 (only in a -DIVFPQ_OVERLAP=1 build) = {args.steps} steps with two "
-                         f"batches in flight on two streams (experimental, not the value: 2 in 24000 such batches "
-                         f"differed from the oracle, profiles/r04_race_rate.jsonl); "
-                         f"host_search = search() on numpy "
+        extra["note"] = (f"{n_ex} batches each; k100 = search_device with k=100 and {inflight} batches in flight "
+                         f"(k100_serial: one at a time on one stream); host_search = search() on numpy "
                          f"queries (H2D copy, search, D2H copy; synchronous)")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -303,14 +293,17 @@ def main():
             Dm, Im = merged[b]
             agree += int(((Im == Ir).all(dim=1) & (Dm == Dr).all(dim=1)).sum().item())
             rows += B
-        for b in range(args.warmup):
-            ix_rep.search_device(mine[b % args.nbatches], k, Dbuf[:B], Ibuf[:B])
+        ix_rep.inflight = inflight > 1
+        for b in range(max(args.warmup, inflight)):
+            j = b % inflight
+            ix_rep.search_device(mine[b % args.nbatches], k, Dbufs[j][:B], Ibufs[j][:B], stream=streams[j].cuda_stream)
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for s in range(args.steps):
-            ix_rep.search_device(mine[s % args.nbatches], k, Dbuf[:B], Ibuf[:B])
+        for s in range(args.steps):  # the same batches in flight as the sharded value
+            j = s % inflight
+            ix_rep.search_device(mine[s % args.nbatches], k, Dbufs[j][:B], Ibufs[j][:B], stream=streams[j].cuda_stream)
         torch.cuda.synchronize()
         dist.barrier()
         tr = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)

@@ -209,7 +209,7 @@ __device__ __forceinline__ void copy_code(uint8_t* __restrict__ d, const uint8_t
 // t + |{o in O : o <= label_t}|; when every new label is above the old ones (ids
 // assigned sequentially) both counts are trivial and the list is an append.
 constexpr int kTile = 65536;
-__global__ __launch_bounds__(256) void k_merge_lists(int lo, const int64_t* __restrict__ old_off,
+__global__ __launch_bounds__(256) void k_merge_lists(int lo, int hi, const int64_t* __restrict__ old_off,
                                                      const uint8_t* __restrict__ old_codes,
                                                      const int64_t* __restrict__ old_ids,
                                                      const int64_t* __restrict__ new_off,
@@ -217,28 +217,30 @@ __global__ __launch_bounds__(256) void k_merge_lists(int lo, const int64_t* __re
                                                      const int64_t* __restrict__ new_ids,
                                                      const int64_t* __restrict__ out_off, int M,
                                                      uint8_t* __restrict__ out_codes, int64_t* __restrict__ out_ids) {
-  const int l = lo + blockIdx.y;
-  const int64_t ob = old_off[l], no = old_off[l + 1] - ob;
-  const int64_t nb = new_off[l], nn = new_off[l + 1] - nb;
-  const int64_t t0 = (int64_t)blockIdx.x * kTile;
-  if (t0 >= no + nn) return;
-  const int64_t dst = out_off[l];
-  const int64_t* O = old_ids + ob;
-  const int64_t* N = new_ids + nb;
-  const bool append = nn == 0 || no == 0 || O[no - 1] < N[0];
-  const int64_t t1 = min(t0 + kTile, no + nn);
-  for (int64_t e = t0 + threadIdx.x; e < t1; e += 256) {
-    if (e < no) {  // old entry r = e
-      const int64_t lab = O[e];
-      const int64_t at = dst + e + (append ? 0 : bsearch_i64(N, nn, lab, false));
-      copy_code(out_codes + at * M, old_codes + (ob + e) * M, M);
-      out_ids[at] = lab;
-    } else {  // new entry t = e - no
-      const int64_t t = e - no;
-      const int64_t lab = N[t];
-      const int64_t at = dst + t + (append ? no : bsearch_i64(O, no, lab, true));
-      copy_code(out_codes + at * M, new_codes + (nb + t) * M, M);
-      out_ids[at] = lab;
+  // lists beyond gridDim.y (at most 65535 rows) are taken in strides of it
+  for (int l = lo + blockIdx.y; l < hi; l += gridDim.y) {
+    const int64_t ob = old_off[l], no = old_off[l + 1] - ob;
+    const int64_t nb = new_off[l], nn = new_off[l + 1] - nb;
+    const int64_t t0 = (int64_t)blockIdx.x * kTile;
+    if (t0 >= no + nn) continue;
+    const int64_t dst = out_off[l];
+    const int64_t* O = old_ids + ob;
+    const int64_t* N = new_ids + nb;
+    const bool append = nn == 0 || no == 0 || O[no - 1] < N[0];
+    const int64_t t1 = min(t0 + kTile, no + nn);
+    for (int64_t e = t0 + threadIdx.x; e < t1; e += 256) {
+      if (e < no) {  // old entry r = e
+        const int64_t lab = O[e];
+        const int64_t at = dst + e + (append ? 0 : bsearch_i64(N, nn, lab, false));
+        copy_code(out_codes + at * M, old_codes + (ob + e) * M, M);
+        out_ids[at] = lab;
+      } else {  // new entry t = e - no
+        const int64_t t = e - no;
+        const int64_t lab = N[t];
+        const int64_t at = dst + t + (append ? no : bsearch_i64(O, no, lab, true));
+        copy_code(out_codes + at * M, new_codes + (nb + t) * M, M);
+        out_ids[at] = lab;
+      }
     }
   }
 }
@@ -258,8 +260,8 @@ hipError_t image_merge_lists(const ListMergeArgs& g, hipStream_t s) {
   hipLaunchKernelGGL(k_sum_offsets, dim3(nblk(g.nlist + 1, 256)), dim3(256), 0, s, g.old_off, g.new_off, g.nlist,
                      g.out_off);
   if (g.hi > g.lo && g.max_list > 0) {
-    const dim3 grid((unsigned)((g.max_list + kTile - 1) / kTile), (unsigned)(g.hi - g.lo));
-    hipLaunchKernelGGL(k_merge_lists, grid, dim3(256), 0, s, g.lo, g.old_off, g.old_codes, g.old_ids, g.new_off,
+    const dim3 grid((unsigned)((g.max_list + kTile - 1) / kTile), (unsigned)std::min(g.hi - g.lo, 65535));
+    hipLaunchKernelGGL(k_merge_lists, grid, dim3(256), 0, s, g.lo, g.hi, g.old_off, g.old_codes, g.old_ids, g.new_off,
                        g.new_codes, g.new_ids, g.out_off, g.M, g.out_codes, g.out_ids);
   }
   return hipGetLastError();

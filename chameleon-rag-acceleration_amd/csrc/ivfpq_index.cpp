@@ -234,6 +234,7 @@ struct ivfpq_index {
   uint64_t uses = 0;
   bool inflight = inflight_default();
   int fault_inj = 0;  // test hook (ivfpq_set_fault_injection): ListPlan::fault
+  std::vector<uint64_t> tau_seed;  // test hook (ivfpq_debug_seed_tau): the next batch's starting bounds
   std::mutex mu;
 
   Work& W() { return work[slot]; }
@@ -323,6 +324,13 @@ struct ivfpq_index {
       if (w.done_pending) HIPCHECK(hipEventSynchronize(w.done));
       HIPCHECK(hipMemsetAsync(w.p_tau.p, 0xff, w.p_tau.bytes, s));
       w.epoch = 1;
+    }
+    if (!tau_seed.empty()) {  // one-shot: this batch starts with the seeded bounds (its own tag)
+      require((int64_t)tau_seed.size() == nq, "seeded bounds: one per query of the next batch");
+      for (auto& v : tau_seed) v = ((uint64_t)(~w.epoch) << 32) | (uint32_t)v;
+      HIPCHECK(hipMemcpyAsync(w.p_tau.p, tau_seed.data(), sizeof(uint64_t) * nq, hipMemcpyHostToDevice, s));
+      HIPCHECK(hipStreamSynchronize(s));
+      tau_seed.clear();
     }
     pl.qmw = (np + 63) / 64;
     w.p_qmask.ensure(sizeof(uint64_t) * nq * pl.qmw);
@@ -1250,7 +1258,7 @@ int ivfpq_set_list_range(ivfpq_index* h, int lo, int hi) {
     check_handle(h);
     std::lock_guard<std::mutex> lk(h->mu);
     require(0 <= lo && lo <= hi && hi <= h->nlist, "invalid list range");
-    require(h->ntotal == 0, "set the list range before adding vectors");
+    require(h->ntotal == 0 && h->q_n == 0, "set the list range before adding vectors");
     h->list_lo = lo;
     h->list_hi = hi;
     h->dirty = true;  // the device image (list order) follows the range
@@ -1432,6 +1440,21 @@ int ivfpq_set_fault_injection(ivfpq_index* h, int every) {
     std::lock_guard<std::mutex> lk(h->mu);
     require(every >= 0, "fault injection period must be >= 0");
     h->fault_inj = every;
+  });
+}
+
+int ivfpq_debug_seed_tau(ivfpq_index* h, int64_t n, const float* keys) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    require(n >= 0 && (n == 0 || keys), "null buffer");
+    h->tau_seed.resize(n);
+    for (int64_t i = 0; i < n; i++) {  // the ordered-int word of the key (ivfpq_kernels.hip tau_lower)
+      int32_t b;
+      std::memcpy(&b, keys + i, 4);
+      const int32_t o = b >= 0 ? b : b ^ 0x7FFFFFFF;
+      h->tau_seed[i] = (uint32_t)o ^ 0x80000000u;
+    }
   });
 }
 

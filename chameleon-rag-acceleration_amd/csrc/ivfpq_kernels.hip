@@ -595,7 +595,14 @@ __device__ __forceinline__ void plan_pair(const ListPlan& pl, int nloc, int64_t 
 // must not be served from a non-coherent cached copy.
 __device__ __forceinline__ int tau_get(const ListPlan& pl, int64_t q) {
   const uint64_t v = __hip_atomic_load(pl.tauq + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (uint32_t)(v >> 32) == ~pl.epoch ? (int)((uint32_t)v ^ 0x80000000u) : f2ord(kInf);
+  // One value for the whole wave.  The lanes' loads of this word are separate
+  // requests, and another workgroup's atomicMin can land between them: lanes would
+  // then hold different bounds, and every "wave-uniform" branch on the bound
+  // (loose / fast admission / queue fills) would diverge -- the wrong-rows failure
+  // under concurrent kernels ("Uniform bounds").
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  return hi == ~pl.epoch ? (int)(lo ^ 0x80000000u) : f2ord(kInf);
 }
 // tau_q := min(tau_q, o) within this batch (any k real candidates bound the final k-th key)
 __device__ __forceinline__ void tau_lower(const ListPlan& pl, int64_t q, int o) {
@@ -2299,7 +2306,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
       loose = false;
 #pragma unroll
       for (int g = 0; g < G; g++) {
-        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));
+        // (readfirstlane: one value for the wave, as tau_get -- the two 32-lane halves of
+        // the LDS read can straddle another wave's atomicMin)
+        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(__builtin_amdgcn_readfirstlane(s_wb[g])));
         loose = loose || bound[g] == kInf;
       }
       DIAG_ONLY(const uint64_t tb0 = __builtin_amdgcn_s_memtime(); d_loose += tb0 - tg0;)

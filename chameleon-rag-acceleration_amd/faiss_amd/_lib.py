@@ -47,6 +47,7 @@ SIGNATURES = {
     "ivfpq_set_fault_injection": (ctypes.c_int, [c_handle, ctypes.c_int]),
     "ivfpq_debug_workspace": (ctypes.c_int, [c_handle, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
                                              c_i64p]),
+    "ivfpq_debug_seed_tau": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p]),
     "ivfpq_add_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
     "ivfpq_add_preencoded": (ctypes.c_int, [c_handle, ctypes.c_int64, c_i64p, c_u8p, c_i64p]),

@@ -173,6 +173,10 @@ int ivfpq_set_fault_injection(ivfpq_index* h, int every);
  * masks, 3 tau words, 4 header words, 5 coarse lists, 6 coarse dis0; 7 / 8: the epoch of the
  * last batch planned there / the stream it ran on (8 bytes each); *bytes = its size. */
 int ivfpq_debug_workspace(ivfpq_index* h, int ws, int what, void* dst, int64_t cap, int64_t* bytes);
+/* Test hook for the cross-workgroup bound: the next device search (of exactly n queries)
+ * starts with query i's shared bound tau_i = keys[i] instead of +inf (one-shot).  Any
+ * keys[i] >= that query's true k-th key is a valid bound, and results must not change. */
+int ivfpq_debug_seed_tau(ivfpq_index* h, int64_t n, const float* keys);
 
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing

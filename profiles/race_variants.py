@@ -221,7 +221,7 @@ def notau(s):  # no cross-workgroup bound: tau_q never read (every item starts u
 
 
 def nowb(s):  # no cross-wave bound inside an item (s_wb never read)
-    return sub(s, "        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(s_wb[g]));",
+    return sub(s, "        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(__builtin_amdgcn_readfirstlane(s_wb[g])));",
                "        (void)s_wb;")
 
 

@@ -409,9 +409,6 @@ def test_precomputed_tables_with_batches_in_flight(sift1m, inflight):
     Every batch equals its plain preassigned search."""
     import torch
 
-    if inflight and not faiss.overlap_built():
-        pytest.skip("the batches-in-flight overlap is not built (-DIVFPQ_OVERLAP=1)")
-
     ix, ox, xq = sift1m
     ix.nprobe = 16
     B = 256

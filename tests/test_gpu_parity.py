@@ -264,28 +264,18 @@ def rr_index():
     return ix, xq
 
 
-@pytest.mark.parametrize("inflight", [
-    False,
-    # the experimental overlap mode (not built by default): about 1 in
-    # 10^4 overlapped k = 10 batches differs from its search alone (profiles/r04_race_rate.jsonl:
-    # 2 / 24000 at 2 streams, 14 / 24000 at 3; ordered: 0 / 24000), so this 96-batch case
-    # fails in a few percent of runs of a -DIVFPQ_OVERLAP=1 build; the ordered case is the gate
-    pytest.param(True, marks=pytest.mark.xfail(strict=False, reason="overlap mode: rare mismatch, DESIGN.md 4")),
-])
+@pytest.mark.parametrize("inflight", [False, True])
 def test_batches_in_flight_on_round_robin_streams(rr_index, inflight):
     """24 batches issued round robin on 2, 3, 4 and 5 streams with no
     synchronisation, at k = 10 (row-packed scan) and k = 100 (k > 64 merge), with
     a coarse_device + preassigned search interleaved, in both stream modes:
     searches ordered across streams, and batches in flight (k = 10: up to three
-    overlapping in per-stream workspaces, 4 and 5 streams take workspaces over;
-    k = 100 searches are ordered in both modes, ivfpq_index.cpp kInflightMaxK).
+    overlapping in per-stream workspaces, 4 and 5 streams take workspaces over).
     Every batch equals its search alone on one stream, bit for bit (those are
     checked against the oracle for the first batch), and the merge kernels'
     index checks count nothing."""
     import torch
 
-    if inflight and not faiss.overlap_built():
-        pytest.skip("the batches-in-flight overlap is not built (-DIVFPQ_OVERLAP=1)")
     ix, xq = rr_index
     nb = 24
     xd = torch.from_numpy(xq).cuda().view(nb, 256, 64)
@@ -330,6 +320,45 @@ def test_batches_in_flight_on_round_robin_streams(rr_index, inflight):
             np.testing.assert_array_equal(pre[1].cpu().numpy(), ref[5][1])
             np.testing.assert_array_equal(pre[0].cpu().numpy(), ref[5][0])
     assert ix.error_count() == 0
+
+
+@pytest.mark.parametrize("k,nst", [(10, 3), (100, 2), (100, 3)])
+def test_batches_in_flight_stress(rr_index, k, nst):
+    """The concurrent-kernel regression ("Uniform bounds"): 40
+    rounds of 24 batches in flight on nst streams -- before the wave-uniform bound fix
+    about 1 batch in 1700 (k = 10, 3 streams) to 1 in 60 (k = 100, 2 streams) lost a
+    true neighbour here (profiles/r05_ab/, profiles/r05_race_inflight.jsonl).  Every
+    batch must equal its search alone, with no index-check or stale-entry events."""
+    import torch
+
+    ix, xq = rr_index
+    nb = 24
+    xd = torch.from_numpy(xq).cuda().view(nb, 256, 64)
+    ref = []
+    for b in range(nb):
+        D, I = ix.search_device(xd[b], k)
+        torch.cuda.synchronize()
+        ref.append((D.cpu().numpy(), I.cpu().numpy()))
+    streams = [torch.cuda.Stream() for _ in range(nst)]
+    e0 = ix.error_count()
+    bad = []
+    for rnd in range(40):
+        outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
+                for _ in range(nb)]
+        ix.inflight = True
+        try:
+            torch.cuda.synchronize()
+            for b in range(nb):
+                ix.search_device(xd[b], k, outs[b][0], outs[b][1], stream=streams[b % nst].cuda_stream)
+            torch.cuda.synchronize()
+        finally:
+            ix.inflight = False
+        for b in range(nb):
+            if not (np.array_equal(outs[b][1].cpu().numpy(), ref[b][1])
+                    and np.array_equal(outs[b][0].cpu().numpy(), ref[b][0])):
+                bad.append((rnd, b))
+    assert not bad, f"{len(bad)} of {40 * nb} batches differ: {bad[:8]}"
+    assert ix.error_count() == e0
 
 
 def test_device_entry_points_reject_bad_tensors(golden_dir):
