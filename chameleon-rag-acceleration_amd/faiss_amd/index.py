@@ -494,10 +494,9 @@ class IndexIVFPQ:
         """Batches in flight: True lets device searches issued on different
         streams overlap (each stream keeps its own workspace, up to three);
         False (default, unless IVFPQ_INFLIGHT=1 at creation) orders each search
-        after those still in flight on other streams.  The overlap is
-        experimental and only in a library built with -DIVFPQ_OVERLAP=1
-        (``overlap_built()``): about 1 overlapped batch in 10^4 differs from the
-        oracle; setting True otherwise raises."""
+        after those still in flight on other streams.  Results are the same in
+        both modes (tests/test_gpu_parity.py
+        test_batches_in_flight_stress)."""
         return bool(_lib.load().ivfpq_get_inflight(self._h))
 
     @inflight.setter
