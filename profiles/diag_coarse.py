@@ -24,9 +24,10 @@ def main():
     from faiss_amd import _lib, datasets
 
     nb = int(os.environ.get("NB", "1000000"))
-    xt = datasets.synthetic_sift_like(100_000, 128, seed=4321)
-    xb = datasets.synthetic_sift_like(nb, 128, seed=1234)
-    xq = datasets.synthetic_sift_like(1024, 128, seed=123)
+    gen = dict(n_centres=200_000)  # bench.py's data
+    xt = datasets.synthetic_sift_like(100_000, 128, seed=4321, **gen)
+    xb = datasets.synthetic_sift_like(nb, 128, seed=1234, **gen)
+    xq = datasets.synthetic_sift_like(1024, 128, seed=123, **gen)
     ix = faiss.index_factory(128, "IVF1024,PQ16")
     ix.train(xt)
     ix.add(xb)
@@ -65,6 +66,12 @@ def main():
             print(f"  {nm:13s} mean {v.mean():8.0f} p50 {np.median(v):8.0f} p90 {np.percentile(v, 90):8.0f} max {v.max():8.0f}")
         tot = (a[:, :, 5] - a[:, :, 0])[ok]
         print(f"  total         mean {tot.mean():8.0f} max {tot.max():8.0f} cycles")
+        allok = (a[:, :, 0] > 0) & (a[:, :, 5] > 0)
+        t0 = a[:, :, 0][allok].min()
+        st, en = (a[:, :, 0] - t0)[ok], (a[:, :, 5] - t0)[ok]
+        q = [0, 10, 50, 90, 100]
+        print("  start (from the first wave) p0/10/50/90/100", [int(np.percentile(st, x)) for x in q])
+        print("  end                          p0/10/50/90/100", [int(np.percentile(en, x)) for x in q])
 
 
 if __name__ == "__main__":
