@@ -2718,14 +2718,17 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     const bool scanned = (lane >> 2) < np && ((pl.qmask[q] >> p) & 1);
     const int64_t slot = (q * np + p) * 4 + (lane & 3);
     const uint32_t expect = part_tag(pl.epoch, slot);
-    // unconditional, clamped loads (no divergent branch around them); slots of
-    // unscanned probes (empty or foreign lists, lanes past nprobe) were never
-    // written this batch: their contents are stale and must not be used
+    // clamped loads, only for scanned probes: slots of unscanned probes (empty or
+    // foreign lists, lanes past nprobe) were never written this batch (their
+    // contents are stale and must not be used), and a list-range shard scans few of
+    // a query's probes -- at N = 8 about 2 of 16, so loading every slot read 8x the
+    // partial lists the scan wrote
     int64_t pos[U];
     bool fresh[U];
+    const uint4 none = make_uint4(__float_as_uint(kInf), expect, 0xFFFFFFFFu, 0xFFFFFFFFu);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint4 r = pl.part[slot * ks + min(u, k - 1)];
+      const uint4 r = scanned ? pl.part[slot * ks + min(u, k - 1)] : none;
       d[u] = rec_key(r);
       pos[u] = rec_pos(r);
       fresh[u] = tag_ok(r.y, expect);
@@ -2747,7 +2750,25 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
       bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; u++) ok[u] = scanned && u < k && pos_ok(a, pl, pos[u]);
-      const float T = wave_kth_smallest(ok[0] ? d[0] : kInf, k, lane);
+      // a bound on the k-th key from m sorted lists: with j = ceil(k / m) - 1, the
+      // i = ceil(k / (j + 1)) smallest of the lists' entries j are each preceded in
+      // their list by j entries, so i (j + 1) >= k entries are at or below the i-th
+      // smallest of them (m >= k: the k-th smallest list head).  A list-range shard
+      // scans few probes of a query (N = 8: about 2 of 16, m = 8 < k), so the
+      // head-only bound left nearly every query to the full merge below.
+      const int m = __popcll(__builtin_amdgcn_ballot_w64(ok[0]));
+      if (m == 0) {  // nothing scanned for this query (every probe empty or outside the range)
+        if (lane < k) {
+          a.outD[q * k + lane] = pad;
+          a.outI[q * k + lane] = -1;
+        }
+        return;
+      }
+      const int jb = (k + m - 1) / m - 1;  // < k <= U (wave-uniform)
+      float vj = kInf;
+#pragma unroll
+      for (int u = 0; u < U; u++) vj = (u == jb && ok[u]) ? d[u] : vj;
+      const float T = wave_kth_smallest(vj, (k + jb) / (jb + 1), lane);
       const uint64_t lt = (1ull << lane) - 1;
       int total = 0;
 #pragma unroll
