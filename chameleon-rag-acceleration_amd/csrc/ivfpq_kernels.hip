@@ -1372,6 +1372,8 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
   for (int p0 = 0; p0 < nprobe; p0 += 64) {
     const int p = p0 + lane;
     const int64_t l = p < nprobe ? lists[q * nprobe + p] : -1;
+    // (L2) dis0 loaded with the probe, not after the range and duplicate checks
+    const float dq = (!ip && Dq && p < nprobe) ? Dq[q * nprobe + p] : 0.f;
     bool use = p < nprobe && l >= lo && l < hi && list_off[l + 1] > list_off[l];
     if (dedup) {
       // an earlier probe with the same list: the earlier ones of this 64-probe
@@ -1392,7 +1394,7 @@ __global__ __launch_bounds__(256) void k_plan_count(const int64_t* __restrict__ 
     float d0 = 0.f;
     if (ip && um) d0 = wave_ip_dis0(x + q * d, cent, use ? l : -1, d, min(64, nprobe - p0), lane);  // (uniform)
     if (use) {
-      if (!ip) d0 = Dq ? Dq[q * nprobe + p] : 0.f;
+      if (!ip) d0 = dq;
       plan_pair(pl, hi - lo, l, lo, lane == fp ? 0 : 1, (int)(q * nprobe + p), d0);
     }
   }
@@ -3405,13 +3407,29 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
 __global__ __launch_bounds__(256) void k_merge_topk(int S, int64_t n, int k, const float* __restrict__ Din,
                                                     const int64_t* __restrict__ Iin, float* __restrict__ Dout,
                                                     int64_t* __restrict__ Iout, int ip) {
+  // the query's S x k entries staged in LDS when they fit (N = 8, k = 10: 80), so the
+  // (S - 1) binary searches of every entry are LDS reads, not dependent global loads
+  constexpr int kStage = 2048;
+  __shared__ float s_d[kStage];
+  __shared__ int64_t s_i[kStage];
   const int64_t q = blockIdx.x;
   const float sgn = ip ? -1.f : 1.f;
-  auto key_d = [&](int s, int j) { return sgn * Din[((int64_t)s * n + q) * k + j]; };
-  auto key_i = [&](int s, int j) {
+  const bool staged = S * k <= kStage;
+  auto gkey_d = [&](int s, int j) { return sgn * Din[((int64_t)s * n + q) * k + j]; };
+  auto gkey_i = [&](int s, int j) {
     const int64_t v = Iin[((int64_t)s * n + q) * k + j];
     return v < 0 ? kSentinelId : v;
   };
+  if (staged) {
+    for (int e = threadIdx.x; e < S * k; e += 256) {
+      const int s = e / k;
+      s_d[e] = gkey_d(s, e - s * k);
+      s_i[e] = gkey_i(s, e - s * k);
+    }
+    __syncthreads();
+  }
+  auto key_d = [&](int s, int j) { return staged ? s_d[s * k + j] : gkey_d(s, j); };
+  auto key_i = [&](int s, int j) { return staged ? s_i[s * k + j] : gkey_i(s, j); };
   for (int e = threadIdx.x; e < S * k; e += 256) {
     const int s = e / k;
     const int idx = e - s * k;
