@@ -106,6 +106,16 @@ def test_add_device_list_range_shard_keeps_its_lists():
     for l in range(64, 160):
         np.testing.assert_array_equal(sh.invlists.get_ids(l), np.flatnonzero(lo == l))
         np.testing.assert_array_equal(sh.invlists.get_codes(l).reshape(-1, 16), co[lo == l])
+    # the range cannot change under pending adds, even when none of them is kept
+    # (ntotal == 0 alone let such a change through)
+    sh2 = faiss.IndexIVFPQ(None, 64, 256, 16, 8, device=0)
+    sh2.set_trained(ix.centroids(), ix.codebook())
+    sh2.set_list_range(0, 1)
+    far = xb[lo >= 1][:100]
+    sh2.add_device(torch.from_numpy(far).cuda())
+    assert sh2.ntotal == 0
+    with pytest.raises(RuntimeError, match="list range"):
+        sh2.set_list_range(0, 256)
     # a reset empties the device image too
     sh.reset()
     assert sh.ntotal == 0 and sh.invlists.list_sizes().sum() == 0
