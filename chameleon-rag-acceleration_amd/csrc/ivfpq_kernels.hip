@@ -2725,12 +2725,15 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     // contents are stale and must not be used), and a list-range shard scans few of
     // a query's probes -- at N = 8 about 2 of 16, so loading every slot read 8x the
     // partial lists the scan wrote
+    // (unconditional loads: an unscanned lane reads the first scanned lane's slot --
+    // the same lines, no extra traffic -- and ignores what it reads)
     int64_t pos[U];
     bool fresh[U];
-    const uint4 none = make_uint4(__float_as_uint(kInf), expect, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    const uint64_t sm = __builtin_amdgcn_ballot_w64(scanned);
+    const int64_t rslot = scanned || !sm ? slot : (int64_t)__builtin_amdgcn_readlane((int)slot, (int)__builtin_ctzll(sm));
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint4 r = scanned ? pl.part[slot * ks + min(u, k - 1)] : none;
+      const uint4 r = pl.part[rslot * ks + min(u, k - 1)];
       d[u] = rec_key(r);
       pos[u] = rec_pos(r);
       fresh[u] = tag_ok(r.y, expect);
