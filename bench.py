@@ -240,7 +240,7 @@ def main():
     # profiling K) on the device path, and the host-buffer search() (PCIe included)
     extra = {}
     if not args.no_extra and not shard:
-        n_ex = max(5, min(20, args.steps))
+        n_ex = max(5, min(50, args.steps))
         D100 = torch.empty((Bg, 100), dtype=torch.float32, device=dev)
         I100 = torch.empty((Bg, 100), dtype=torch.int64, device=dev)
         D100 = [D100] + [torch.empty_like(D100) for _ in range(inflight - 1)]
