@@ -150,6 +150,39 @@ def test_add_device_large_nlist_segmented_assignment():
     np.testing.assert_array_equal(got_c, co)
 
 
+def test_incremental_add_above_65536_lists():
+    """The per-list merge of incremental adds (k_merge_lists) at nlist 70 000: its
+    grid takes at most 65 535 lists per row of workgroups and strides over the rest
+    (ADVICE r04); two device adds with interleaved labels, then every list equals the
+    oracle's entries for both chunks, label-sorted."""
+    import torch
+
+    rng = np.random.default_rng(21)
+    d, nlist, M = 16, 70_000, 8
+    cent = rng.integers(0, 64, size=(nlist, d)).astype(np.float32)
+    cb = rng.standard_normal((M, 256, d // M), dtype=np.float32)
+    ix = faiss.IndexIVFPQ(None, d, nlist, M, 8, device=0)
+    ix.set_trained(cent, cb)
+    ox = O.OracleIVFPQ(d, nlist, M)
+    ox.set_trained(cent, cb)
+    n = 200_000
+    xb = rng.integers(0, 64, size=(n, d)).astype(np.float32)
+    ids = rng.permutation(10 * n)[:n].astype(np.int64)
+    half = n // 2
+    ix.add_with_ids(xb[:half], ids[:half])
+    ix.nprobe = 4
+    ix.search(xb[:8], 5)  # the first chunk is merged into the image here
+    ix.add_with_ids(xb[half:], ids[half:])
+    ix.search(xb[:8], 5)  # the second chunk merges into the existing lists (labels interleave)
+    lo, co = ox.encode(xb)
+    for l in np.unique(lo)[:: max(1, len(np.unique(lo)) // 500)]:
+        sel = np.flatnonzero(lo == l)
+        order = np.argsort(ids[sel], kind="stable")
+        np.testing.assert_array_equal(ix.invlists.get_ids(int(l)), ids[sel][order])
+        np.testing.assert_array_equal(ix.invlists.get_codes(int(l)).reshape(-1, M), co[sel][order])
+    assert int(ix.invlists.list_sizes().sum()) == n
+
+
 @pytest.mark.parametrize("shard", [False, True])
 def test_incremental_adds_in_50k_chunks(shard):
     """beir's FaissIndex.build adds in 50k chunks (beir/beir/retrieval/search/
