@@ -148,6 +148,14 @@ def _collective_worker(rank, world, port, out):
     dist.all_gather(hD, Dq)
     dist.all_gather(hI, Iq)
     ok = ok and torch.equal(aD, torch.cat(hD)) and torch.equal(aI, torch.cat(hI))
+    # bench.py with batches in flight: one process group per in-flight stream, used
+    # alternately; every group gives the same slices as the default one
+    groups = [dist.new_group(list(range(world))) for _ in range(2)]
+    for step in range(4):
+        grp = groups[step % 2]
+        Ds2, Is2 = exchange_partials(Dp, Ip, world, grp)
+        aD2, aI2 = all_gather_probes(Dq, Iq, world, grp)
+        ok = ok and torch.equal(Ds2, Ds) and torch.equal(Is2, Is) and torch.equal(aD2, aD) and torch.equal(aI2, aI)
     flags = [torch.zeros(1) for _ in range(world)]
     dist.all_gather(flags, torch.tensor([1.0 if ok else 0.0]))
     if rank == 0:
@@ -159,7 +167,8 @@ def _collective_worker(rank, world, port, out):
 @pytest.mark.parametrize("world", [2, 4])
 def test_exchange_collectives_slicing(tmp_path, world):
     """The collectives bench.py's shard step runs over RCCL (all_to_all_single of
-    the partials, all_gather_into_tensor of the probes), executed here under gloo:
+    the partials, all_gather_into_tensor of the probes; on the default group and on
+    the per-stream groups of batches in flight), executed here under gloo:
     rank r receives slice r of every rank's partials in rank order, and the
     probes of slice s come from rank s -- the layout of a gather-then-slice
     reference."""
