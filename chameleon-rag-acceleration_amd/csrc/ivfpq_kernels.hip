@@ -885,6 +885,13 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     const int64_t q0 = (int64_t)(tb / t3.M) * GQ;
     const int m = tb % t3.M;
     const int e = m * 256 + tid;
+    // the centroid is loaded before the sub-vectors are staged: one round trip, not two
+    float4 c0 = {}, c1 = {};
+    if (dsub == 8) {
+      const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
+      c0 = src[0];
+      c1 = src[1];
+    }
     float* xs = g_lds;  // [GQ][dsub]: the queries' sub-vectors m
     for (int i = tid; i < GQ * dsub; i += 256) {
       const int qq = i / dsub;
@@ -894,8 +901,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     CDIAG(1);
     const int nqq = (int)min<int64_t>(GQ, nq - q0);
     if (dsub == 8) {
-      const float4* src = reinterpret_cast<const float4*>(t3.cb + (int64_t)e * 8);
-      const float4 c0 = src[0], c1 = src[1];
       const float w[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
 #pragma unroll
       for (int qq = 0; qq < GQ; qq++) {
@@ -922,13 +927,37 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   const int dk = (d + 63) & ~63;  // A rows, zero-padded to whole double chunks
   float* xs = g_lds;              // [dk][GQ]: the A operand, k-major
   float* xn = xs + dk * GQ;       // [GQ]
-  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
-  CDIAG(1);
   f4 acc[NTL];
-  coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
+  const int i16 = lane & 15, k4 = lane >> 4;
+  if (d > 96 && d <= 128) {
+    // (C1/C2, d = 128) every B row this wave uses is loaded before the queries
+    // are staged, so the centroid loads overlap the staging and its barriers: one
+    // global round trip instead of a chain of chunk loads.  Same ascending-k MFMA
+    // chain as coarse_key_tile (rows past d clamped, their A entries 0).
+    float b[32][NTL];
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const int64_t kr = min(4 * j + k4, d - 1);
+#pragma unroll
+      for (int t = 0; t < NTL; t++) b[j][t] = centT[kr * ldc + min(c0 + t * 16 + i16, nlist - 1)];
+    }
+    coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+    CDIAG(1);
+#pragma unroll
+    for (int t = 0; t < NTL; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const float av = xs[(4 * j + k4) * GQ + i16];
+#pragma unroll
+      for (int t = 0; t < NTL; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
+    }
+  } else {
+    coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+    CDIAG(1);
+    coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
+  }
   CDIAG(2);
   __syncthreads();  // xn
-  const int i16 = lane & 15, k4 = lane >> 4;
 #pragma unroll
   for (int t = 0; t < NTL; t++) {
     const int c = c0 + t * 16 + i16;
