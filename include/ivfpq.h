@@ -28,7 +28,7 @@
  * Results under concurrent GPU work: the same in both modes and beside other
  * kernels on the GPU.  Round 4's rare wrong rows under concurrent kernels came
  * from per-lane reads of the scan's shared bounds ("Uniform
- * bounds"; fixed in round 5, 0 of 590 400 stressed batches since).  Every per-wave
+ * bounds"; fixed in round 5, 0 of 1 046 400 stressed batches since).  Every per-wave
  * partial list the merge reads is also a set of tagged records (batch epoch +
  * slot): an entry this batch's scan did not leave there is never used -- its probe
  * is rescanned on the device by the merge -- and such events are counted
