@@ -81,6 +81,15 @@ def parse():
                    help="Gaussian centres of the synthetic generator (200k: the recall curve tracks SIFT1M's; "
                         "rounds 1-2 used 10k)")
     p.add_argument("--mode", choices=["shard", "replicas"], default="shard")
+    p.add_argument("--shard-at-1", action="store_true",
+                   help="run the list-range shard flow at WORLD_SIZE=1 too, with a real nccl (RCCL) process group of "
+                        "one rank: every collective of the N > 1 step is a real RCCL call and its communicator stream "
+                        "exists (the stream topology the scaling run uses, measured on one GPU)")
+    p.add_argument("--comms", choices=["one", "per-stream"], default="one",
+                   help="shard flow: one communicator for every in-flight stream (default; the loop issues each "
+                        "batch's all_to_all after the next batch's all_gather, so the communicator's stream never "
+                        "holds a batch behind another's scan) or one per in-flight stream")
+    p.add_argument("--no-peak", action="store_true", help="skip the HBM stream-copy peak measurement")
     p.add_argument("--cpu-sample", type=int, default=10240, help="queries in the CPU-baseline sample")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget (repetitions)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -110,7 +119,13 @@ def main():
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
+    shard = args.mode == "shard" and (world > 1 or args.shard_at_1)
+    if world > 1 or shard:
+        if world == 1:  # --shard-at-1: a one-rank RCCL group on the loopback rendezvous
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     import faiss_amd as faiss
@@ -118,7 +133,6 @@ def main():
     from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials
 
     t_setup = time.time()
-    shard = world > 1 and args.mode == "shard"
     B = args.batch
     Bg = B * world if shard else B  # queries per step on each rank
     log(f"rank {rank}/{world} generating data nb={args.nb} nt={args.nt}")
@@ -154,9 +168,16 @@ def main():
     k = args.k
     inflight = max(1, args.inflight)
     ix.inflight = inflight > 1
-    # sharded: one communicator per in-flight stream, so that the collectives of two
-    # batches in flight never share one (every rank creates them in the same order)
-    groups = [dist.new_group(list(range(world))) for _ in range(inflight)] if shard else None
+    # Streams of the timed region, per process: `inflight` compute
+    # streams, plus, sharded, the communicator streams of RCCL -- one communicator (the
+    # default group) for every in-flight stream, or (--comms per-stream) one each.  No
+    # side streams: T3 of the global batch rides in the coarse launch of the batch's own
+    # stream (coarse_tables_device).
+    if shard:
+        groups = ([dist.new_group(list(range(world))) for _ in range(inflight)] if args.comms == "per-stream"
+                  else [dist.group.WORLD] * inflight)
+    else:
+        groups = None
     streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
     Dbufs = [torch.empty((Bg, k), dtype=torch.float32, device=dev) for _ in range(inflight)]
     Ibufs = [torch.empty((Bg, k), dtype=torch.int64, device=dev) for _ in range(inflight)]
@@ -173,36 +194,91 @@ def main():
     bytes_lists = bytes_alg
 
     merged = {}
-    sides = [torch.cuda.Stream(dev) for _ in range(inflight)] if shard else None
+    pend = [None] * inflight  # sharded: the batch whose partials stream j has not exchanged yet
+
+    def front(b, j):
+        # coarse of this rank's slice + T3 of the global batch (one launch), probes
+        # all-gathered, this rank's lists scanned for the whole batch -- all on stream j
+        xg = xq_dev[b]
+        with torch.cuda.stream(streams[j]):
+            Dq_s, Iq_s, tok = ix.coarse_tables_device(xg[rank * B:(rank + 1) * B], xg)
+            Dq, Iq = all_gather_probes(Dq_s, Iq_s, world, groups[j], force=True)
+            Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j], tables=tok)
+        pend[j] = (b, Dp, Ip)
+
+    def back(j):
+        # the partials of stream j's batch to their owners, merged on the GPU
+        b, Dp, Ip = pend[j]
+        pend[j] = None
+        with torch.cuda.stream(streams[j]):
+            Ds, Is = exchange_partials(Dp, Ip, world, groups[j], force=True)
+            merged[b] = faiss.merge_topk_device(Ds, Is)
 
     def step(b, j=0):
-        if shard:  # coarse for this rank's slice, probes all-gathered, own lists scanned for the batch
-            xg = xq_dev[b]
-            with torch.cuda.stream(streams[j]):  # collectives and kernels of this batch on stream j
-                # T3 of the global batch on a side stream, concurrent with the coarse step and the all_gather
-                sides[j].wait_stream(streams[j])
-                tok = ix.precompute_tables_device(xg, stream=sides[j].cuda_stream)
-                Dq_s, Iq_s = ix.coarse_device(xg[rank * B:(rank + 1) * B])
-                Dq, Iq = all_gather_probes(Dq_s, Iq_s, world, groups[j])
-                Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j], tables=tok)
-                Ds, Is = exchange_partials(Dp, Ip, world, groups[j])
-                merged[b] = faiss.merge_topk_device(Ds, Is)
+        if shard:
+            # stream j's previous batch is exchanged first, then this batch's front half:
+            # on a shared communicator the order is ... all_gather(s-1), all_to_all(s-2),
+            # all_gather(s), ... so batch s waits only for batch s-2's scan, never s-1's
+            if pend[j] is not None:
+                back(j)
+            front(b, j)
         else:  # stream j of the in-flight set, with its own output buffers
             ix.search_device(xq_dev[b], k, Dbufs[j], Ibufs[j], stream=streams[j].cuda_stream)
 
+    def drain():
+        for j in range(inflight):
+            if pend[j] is not None:
+                back(j)
+
+    def serial_step(b):  # one batch at a time on stream 0
+        step(b, 0)
+        drain()
+
     for j in range(inflight):  # setup: each in-flight stream's workspace allocated, whatever --warmup is
         step(j % args.nbatches, j)
+    drain()
     torch.cuda.synchronize()
     for w in range(args.warmup):
         step(w % args.nbatches, w % inflight)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+
+    # the box's measured HBM peak (STREAM copy and a read sweep, 2 GiB each, best of 10),
+    # beside the nominal 8 TB/s
+    peak_measured = None
+    if not args.no_peak:
+        try:
+            import ctypes
+
+            hl = ctypes.CDLL(os.path.join(REPO, "chameleon-rag-acceleration_amd", "lib", "libhbmstream.so"))
+            nbytes = 2 << 30
+            src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).random_(0, 1 << 30)
+            dst = torch.empty_like(src)
+            sink = torch.empty(1 << 22, dtype=torch.int32, device=dev)
+            cms, rms = ctypes.c_float(0), ctypes.c_float(0)
+            rc = hl.hbm_stream_measure(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                       ctypes.c_int64(nbytes), ctypes.c_void_p(sink.data_ptr()),
+                                       ctypes.c_int64(sink.numel() * 4), 10,
+                                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream),
+                                       ctypes.byref(cms), ctypes.byref(rms))
+            if rc == 0:
+                peak_measured = {"copy_GBps": 2 * nbytes / (cms.value * 1e-3) / 1e9,
+                                 "read_GBps": nbytes / (rms.value * 1e-3) / 1e9,
+                                 "copy_ms": cms.value, "read_ms": rms.value, "bytes": nbytes,
+                                 "kernel": "csrc/hbm_stream.hip (16 B per lane, nontemporal, 8 workgroups per CU, "
+                                           "best of 10; copy counts read + written bytes)"}
+            del src, dst, sink
+            torch.cuda.synchronize()
+        except OSError as e:
+            log(f"hbm peak not measured: {e}")
     log(f"setup {time.time() - t_setup:.1f}s; timing {args.steps} steps")
 
     # timed region: HIP events around the list-scan kernel only, on every
     # --event-every-th step (each recorded event costs ~6 us of stream time; the
     # full stage split is measured in a separate pass below)
+    rs0 = ix.repair_stats()  # (waits for in-flight searches)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -210,10 +286,12 @@ def main():
     for s in range(args.steps):
         ix.set_timing(s % args.event_every == 0, lists_only=True)
         step(s % args.nbatches, s % inflight)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    rs1 = ix.repair_stats()  # stale partial lists the merge repaired in the timed region: must be 0
     ix.set_timing(False)
     stages = ix.get_timing()
     # the same steps one batch at a time on one stream (reported beside the value)
@@ -223,7 +301,7 @@ def main():
         t1 = time.perf_counter()
         for s in range(args.steps):
             ix.set_timing(s % args.event_every == 0, lists_only=True)
-            step(s % args.nbatches)
+            serial_step(s % args.nbatches)
         torch.cuda.synchronize()
         serial_ms = (time.perf_counter() - t1) * 1000.0 / args.steps
         ix.set_timing(False)
@@ -231,7 +309,7 @@ def main():
     # stage breakdown (untimed pass, one stream, every stage bracketed by events)
     ix.set_timing(True)
     for s in range(args.steps):
-        step(s % args.nbatches)
+        serial_step(s % args.nbatches)
     torch.cuda.synchronize()
     ix.set_timing(False)
     stage_split = ix.get_timing()
@@ -276,7 +354,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    if shard:
+    # (a full replica of the index on every rank: only where it fits beside the shard)
+    rep_fits = args.nb * (args.M + 8) < (32 << 30)
+    if shard and not args.no_extra and rep_fits:
         # Beside the sharded value: query-sharded replicas (every rank the whole index,
         # its own slice of each global batch) on the same ranks, and the sharded results
         # checked against the replica's search of the same queries (bit for bit).
@@ -287,7 +367,7 @@ def main():
         mine = [xq_dev[b][rank * B:(rank + 1) * B].contiguous() for b in range(args.nbatches)]
         agree, rows = 0, 0
         for b in range(args.nbatches):
-            step(b)
+            serial_step(b)
             Dr, Ir = ix_rep.search_device(mine[b], k)
             torch.cuda.synchronize()
             Dm, Im = merged[b]
@@ -323,15 +403,10 @@ def main():
     scan_avg_ms = scan_ms / max(scan_n, 1)
     lists_ms, lists_n = stages["lists"]
     bytes_per_step = sum(bytes_alg[s % args.nbatches] for s in range(args.steps)) / args.steps
-    if lists_n > 0:  # list-major path: the dominant kernel is k_scan_lists
-        kernel = f"k_scan_lists<{args.M},...> (list-major LUT + PQ scan + top-k, every probe)"
-        avg_launch_ms = lists_ms / lists_n
-        timed = [s for s in range(args.steps) if s % args.event_every == 0]  # the steps with events
-        bytes_per_launch = sum(bytes_lists[s % args.nbatches] for s in timed) / len(timed)
-    else:  # IVFPQ_SCAN=query: one fused query-major kernel
-        kernel = f"k_scan_topk<{args.M},...> (query-major fused LUT + PQ scan + top-k)"
-        avg_launch_ms = scan_avg_ms
-        bytes_per_launch = bytes_per_step
+    kernel = f"k_scan_lists<{args.M},...> (list-major LUT + PQ scan + top-k, every probe)"
+    avg_launch_ms = lists_ms / max(lists_n, 1)
+    timed = [s for s in range(args.steps) if s % args.event_every == 0]  # the steps with events
+    bytes_per_launch = sum(bytes_lists[s % args.nbatches] for s in timed) / len(timed)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     overlapped = None
     measured_on = "the timed region (one batch at a time)"
@@ -447,7 +522,7 @@ def main():
     traffic = None
     traffic_src = "no counter file"
     config_key = (f"nb{args.nb}-d{args.d}-IVF{args.nlist}-PQ{args.M}-np{args.nprobe}-k{k}-B{B}-w{world}-"
-                  f"{args.mode if world > 1 else 'single'}"
+                  f"{args.mode if world > 1 else ('shard-at-1' if shard else 'single')}"
                   f"-c{args.centres}")
     sha = lib_sha256()
     from faiss_amd import _lib
@@ -485,7 +560,8 @@ def main():
             "config": {
                 "workload": f"IVF{args.nlist},PQ{args.M}x8 search, d={args.d}, nb={args.nb}, nprobe={args.nprobe}, "
                             f"k={k}, batch={B} queries per GPU per step",
-                "parallelism": (f"list-range shards x{world} + RCCL all_to_all merge" if shard
+                "parallelism": (f"list-range shards x{world} + RCCL all_gather / all_to_all ({args.comms} "
+                                f"communicator{'s' if args.comms == 'per-stream' else ''})" if shard
                                 else f"replicas x{world}" if world > 1 else "single GPU"),
                 "global_batch": B * world,
                 "inflight": inflight,
@@ -497,6 +573,9 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
+                "peak_measured": peak_measured["copy_GBps"] if peak_measured else None,
+                "frac_measured": achieved / peak_measured["copy_GBps"] if peak_measured else None,
+                "peak_measured_detail": peak_measured,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "lib_sha256": sha,
@@ -511,13 +590,15 @@ def main():
                 "end_to_end": {"alg_bytes": bytes_per_step, "ms_per_step": ms_per_step,
                                "achieved": bytes_per_step / (ms_per_step * 1e-3) / 1e9 if world == 1 else None},
             },
+            "repairs": rs1[1] - rs0[1],
+            "stale_reads": rs1[0] - rs0[0],
             "stages_ms_per_step": {s: v[0] / max(v[1], 1) for s, v in stage_split.items()},
             "recall": recall,
             "cpu_baseline": cpu_baseline,
             "extra": extra or None,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "ivfpq.h"
+#include "ivfpq_test.h"  // the test hooks are defined here too (not part of the drop-in header)
 #include "ivfpq_kernels.h"
 #include "ivfpq_build.h"
 
@@ -326,11 +327,14 @@ struct ivfpq_index {
       w.epoch = 1;
     }
     if (!tau_seed.empty()) {  // one-shot: this batch starts with the seeded bounds (its own tag)
-      require((int64_t)tau_seed.size() == nq, "seeded bounds: one per query of the next batch");
-      for (auto& v : tau_seed) v = ((uint64_t)(~w.epoch) << 32) | (uint32_t)v;
-      HIPCHECK(hipMemcpyAsync(w.p_tau.p, tau_seed.data(), sizeof(uint64_t) * nq, hipMemcpyHostToDevice, s));
+      // disarmed before the check: a mismatched seed fails this search only, not every later one
+      // (the hook applies to single-chunk searches of exactly the seeded size)
+      std::vector<uint64_t> seed;
+      seed.swap(tau_seed);
+      require((int64_t)seed.size() == nq, "seeded bounds: one per query of the next batch (single-chunk searches)");
+      for (auto& v : seed) v = ((uint64_t)(~w.epoch) << 32) | (uint32_t)v;
+      HIPCHECK(hipMemcpyAsync(w.p_tau.p, seed.data(), sizeof(uint64_t) * nq, hipMemcpyHostToDevice, s));
       HIPCHECK(hipStreamSynchronize(s));
-      tau_seed.clear();
     }
     pl.qmw = (np + 63) / 64;
     w.p_qmask.ensure(sizeof(uint64_t) * nq * pl.qmw);
@@ -788,11 +792,18 @@ struct ivfpq_index {
   // built on the matrix cores (with T3out, the same launch builds T3).  With
   // `plan` and nprobe <= 64 the selection also plans the batch and true is
   // returned; otherwise the caller plans with launch_plan_count.
+  // xt / nt (nullable): T3out holds the tables of the queries xt instead of x (the
+  // shard step: keys of this rank's slice, tables of the global batch, one launch)
   bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
-                     const ListPlan* plan = nullptr, float* T3out = nullptr) {
+                     const ListPlan* plan = nullptr, float* T3out = nullptr, const float* xt = nullptr,
+                     int64_t nt = 0) {
+    if (!xt) {
+      xt = x;
+      nt = c;
+    }
     if (nlist >= kSegmentedNlist && np <= 64) {  // large nlist: no [c][nlist] key matrix
       W().w_cand.ensure(sizeof(uint64_t) * c * coarse_segments(c, nlist, d) * np);
-      if (T3out) launch_ip_table(x, c, d, d_cb.as<float>(), M, ksub, T3out, s);
+      if (T3out) launch_ip_table(xt, nt, d, d_cb.as<float>(), M, ksub, T3out, s);
       launch_coarse_segmented(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, np, W().w_cand.as<uint64_t>(),
                               dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo, list_hi, d_cent.as<float>());
       return plan != nullptr;
@@ -800,7 +811,7 @@ struct ivfpq_index {
     W().w_dist.ensure(sizeof(float) * c * nlist);
     W().w_qn.ensure(sizeof(float) * c);
     launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, W().w_dist.as<float>(), s, ip(), T3out,
-                       d_cb.as<float>(), M, W().w_qn.as<float>());
+                       d_cb.as<float>(), M, W().w_qn.as<float>(), xt, nt);
     if (np <= 64) {
       launch_coarse_select(W().w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
                            list_hi, x, d_cent.as<float>(), d);
@@ -919,6 +930,13 @@ struct ivfpq_index {
   // all-gathered), into one of kPreT3 buffers so that batches in flight each have
   // their own.  Returns the token the search takes (ivfpq.h).
   uint64_t tables_dev(int64_t n, const float* x, hipStream_t s) {
+    PreT3& p = take_pre(n, s);
+    launch_ip_table(x, n, d, d_cb.as<float>(), M, ksub, p.buf.as<float>(), s);
+    HIPCHECK(hipGetLastError());
+    return publish_pre(p, n, s);
+  }
+  // A table entry for n queries, ordered on s after its last consumer and producer.
+  PreT3& take_pre(int64_t n, hipStream_t s) {
     require(trained, "index is not trained");
     require(n >= 1, "precompute_tables needs at least one query");
     const int64_t cap = (int64_t)(kChunkBytes / ((size_t)M * ksub * 4));
@@ -940,8 +958,10 @@ struct ivfpq_index {
     if (p.freed_pending && p.freed_stream != s) HIPCHECK(hipStreamWaitEvent(s, p.freed, 0));
     if (p.ready_pending && p.ready_stream != s) HIPCHECK(hipStreamWaitEvent(s, p.ready, 0));
     p.buf.ensure(sizeof(float) * (size_t)n * M * ksub);
-    launch_ip_table(x, n, d, d_cb.as<float>(), M, ksub, p.buf.as<float>(), s);
-    HIPCHECK(hipGetLastError());
+    p.seq = 0;  // (being rewritten: not consumable until published)
+    return p;
+  }
+  uint64_t publish_pre(PreT3& p, int64_t n, hipStream_t s) {
     HIPCHECK(hipEventRecord(p.ready, s));
     p.ready_stream = s;
     p.ready_pending = true;
@@ -952,6 +972,31 @@ struct ivfpq_index {
   // tables computed ahead are meaningless once the codebook changes or the index is reset
   void drop_tables() {
     for (auto& p : pre) p.seq = 0;
+  }
+
+  // The list-range shard step's front half on one stream: the coarse quantizer of
+  // this rank's n queries x and T3 of the nt queries xt of the global batch (the
+  // key workgroups and the table workgroups of one launch at nlist < 8192), the
+  // tables handed to the preassigned search of xt by the returned token.  No side
+  // stream (side streams past the box's four hardware queues cost a
+  // third of the throughput).
+  uint64_t coarse_tables_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, int64_t nt, const float* xt,
+                             hipStream_t s) {
+    require(trained, "index is not trained");
+    require(n >= 1 && nt >= 1, "coarse_tables needs queries");
+    PreT3& p = take_pre(nt, s);
+    begin_slot(s);
+    const int np = eff_nprobe();
+    const int64_t qc = std::max<int64_t>(1, std::min<int64_t>(n, kChunkBytes / ((size_t)nlist * 4)));
+    for (int64_t q0 = 0; q0 < n; q0 += qc) {
+      const int64_t c = std::min(qc, n - q0);
+      const bool with_t3 = q0 == 0;  // the first chunk's launch also builds every table
+      coarse_launch(x + q0 * d, c, np, Dq + q0 * np, Iq + q0 * np, s, nullptr,
+                    with_t3 ? p.buf.as<float>() : nullptr, with_t3 ? xt : nullptr, with_t3 ? nt : 0);
+      HIPCHECK(hipGetLastError());
+    }
+    mark_done(s);
+    return publish_pre(p, nt, s);
   }
 
   void coarse_dev(int64_t n, const float* x, int64_t* Iq, float* Dq, hipStream_t s) {
@@ -1455,6 +1500,18 @@ int ivfpq_debug_seed_tau(ivfpq_index* h, int64_t n, const float* keys) {
       const int32_t o = b >= 0 ? b : b ^ 0x7FFFFFFF;
       h->tau_seed[i] = (uint32_t)o ^ 0x80000000u;
     }
+  });
+}
+
+int ivfpq_coarse_tables_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, float* Dq, int64_t n_tables,
+                               const float* x_tables, void* stream, uint64_t* token) {
+  return guarded([&] {
+    check_handle(h);
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    require(x != nullptr && Iq != nullptr && Dq != nullptr && x_tables != nullptr && token != nullptr,
+            "null pointer argument");
+    *token = h->coarse_tables_dev(n, x, Iq, Dq, n_tables, x_tables, stream ? (hipStream_t)stream : h->stream);
   });
 }
 

@@ -774,6 +774,10 @@ struct CoarseT3 {
   const float* cb = nullptr;
   int M = 0;
   int nblk = 0;  // T3 workgroups
+  // the queries of the tables: the key tiles' own queries, or (the list-range shard
+  // step) the whole global batch while the key tiles cover this rank's slice
+  const float* x = nullptr;
+  int64_t nq = 0;
 };
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -882,6 +886,8 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     const int tb = blockIdx.x - ngemm;
     const int total = t3.M * 256;
     const int dsub = d / t3.M;
+    x = t3.x;
+    nq = t3.nq;
     const int64_t q0 = (int64_t)(tb / t3.M) * GQ;
     const int m = tb % t3.M;
     const int e = m * 256 + tid;
@@ -2635,8 +2641,10 @@ __global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __re
 // re-read result: the reads until the tag was fresh (full merge), or 0xFFFFFFFF
 // when it never was within kSpin reads).
 __device__ __forceinline__ int log_slot(const ListPlan& pl) {
+  // (the counter stops growing once the log is full, so it can never wrap negative)
+  if (__hip_atomic_load(pl.hdr + kHdrLog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kEvLog) return -1;
   const int e = atomicAdd(pl.hdr + kHdrLog, 1);
-  return e < kEvLog ? e : -1;
+  return (e >= 0 && e < kEvLog) ? e : -1;
 }
 __device__ __forceinline__ void log_stale(const ListPlan& pl, int e, int site, int64_t q, int j, int i, uint32_t expect,
                                           uint32_t found, uint32_t keyb, uint32_t spin) {
@@ -2734,6 +2742,9 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   const float pad = a.ip ? -FLT_MAX : FLT_MAX;
   const float sgn = a.ip ? -1.f : 1.f;  // key -> reported value
   const int64_t ks = pl.ks;
+  // this query's stale read already counted (hdr[kHdrStale] counts a query once per
+  // search: the fast path or an earlier k > 64 merge stage that fell back here)
+  bool counted = false;
   if (R == 1 && np * 4 <= 64) {
     // fast path: lane j owns partial list j = (probe j/4, wave j%4), sorted by
     // (key, label).  T = the k-th smallest list head bounds the k-th key (k
@@ -2771,6 +2782,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
 #pragma unroll
     for (int u = U - 1; u >= 0; u--) bad_u = (scanned && u < k && !fresh[u]) ? u : bad_u;
     if (__builtin_amdgcn_ballot_w64(bad_u >= 0)) {  // stale entries: the full merge below re-reads and repairs
+      counted = true;  // (the full merge does not count this query again)
       if (lane == (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(bad_u >= 0))) atomicAdd(pl.hdr + kHdrStale, 1);
       if (bad_u >= 0) {
         const int ev = log_slot(pl);
@@ -2837,10 +2849,11 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
     // query whose candidates fit their buffers and whose lists were all fresh;
     // the rest (ties, stale entries) take the full merge below
     if (np <= 64) {
-      const int done = pl.qdone[q];
+      const int done = pl.qdone[q];  // 1: merged; 2: a stale read (counted), merge here
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) pl.qdone[q] = 0;  // zero for the next batch
-      if (done) return;
+      if (done == 1) return;
+      counted = done == 2;
     }
   }
   // Full merge.  For k > 64 the entries are visited rank-major across the
@@ -2929,7 +2942,7 @@ __global__ __launch_bounds__(256) void k_merge_probes(ScanArgs a, ListPlan pl) {
   }
   if (__builtin_amdgcn_ballot_w64(stale)) {  // (wave-uniform) rescan every probe with a stale entry
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+    if (lane == 0 && !counted) atomicAdd(pl.hdr + kHdrStale, 1);
     for (int w = 0; w < (np + 63) / 64; w++) {
       uint64_t m = s_bad[wave][w];
       while (m) {
@@ -3011,8 +3024,11 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
     lens[j] = n;
     C += n;
   }
-  if (__builtin_amdgcn_ballot_w64(stale)) {  // (uniform)
-    if (lane == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+  if (__builtin_amdgcn_ballot_w64(stale)) {  // (uniform) counted here; k_merge_probes repairs (qdone 2)
+    if (lane == 0) {
+      atomicAdd(pl.hdr + kHdrStale, 1);
+      pl.qdone[q] = 2;
+    }
     return;
   }
   C = wave_sum_i(C);
@@ -3118,8 +3134,11 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
       }
     }
   }
-  if (__builtin_amdgcn_ballot_w64(stale)) {  // (uniform)
-    if (lane == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+  if (__builtin_amdgcn_ballot_w64(stale)) {  // (uniform) counted here; k_merge_probes repairs (qdone 2)
+    if (lane == 0) {
+      atomicAdd(pl.hdr + kHdrStale, 1);
+      pl.qdone[q] = 2;
+    }
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3282,8 +3301,11 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
       }
     }
   }
-  if (__syncthreads_or(stale)) {
-    if (tid == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+  if (__syncthreads_or(stale)) {  // counted here; k_merge_probes repairs (qdone 2)
+    if (tid == 0) {
+      atomicAdd(pl.hdr + kHdrStale, 1);
+      pl.qdone[q] = 2;
+    }
     return;
   }
   // the k-th smallest present key (all of them when there are at most k)
@@ -3359,8 +3381,11 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
       cl[at] = rec_pos(r);
     }
   }
-  if (__syncthreads_or(stale)) {
-    if (tid == 0) atomicAdd(pl.hdr + kHdrStale, 1);
+  if (__syncthreads_or(stale)) {  // counted here; k_merge_probes repairs (qdone 2)
+    if (tid == 0) {
+      atomicAdd(pl.hdr + kHdrStale, 1);
+      pl.qdone[q] = 2;
+    }
     return;
   }
   const int n = s_n;
@@ -3527,14 +3552,19 @@ void launch_select_rows(const float* dist, int64_t nrows, int ncols, int n, floa
 bool coarse_tiled_ok(int d, int64_t nq) { return d % 4 == 0 && d >= 256 && nq >= 64; }
 
 void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
-                        float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M, float* xn_buf) {
+                        float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M, float* xn_buf,
+                        const float* xt, int64_t nt) {
   if (nq <= 0) return;
+  if (!xt) {  // T3 of the key tiles' own queries
+    xt = x;
+    nt = nq;
+  }
   if (xn_buf && coarse_tiled_ok(d, nq)) {  // large d: 64-query x 128-centroid tiles, k-chunks staged in LDS
     if (!ip) launch_row_norms(x, nq, d, xn_buf, s);
     const int ngemm = (int)(nblocks(nq, TQ) * nblocks(nlist, TC));
     // T3 in its own launch: as extra workgroups of this kernel each would hold the
     // GEMM's 54 KB of static LDS, two per CU (C3: 4 096 T3 workgroups, ~0.13 ms)
-    if (T3out) launch_ip_table(x, nq, d, cb, M, 256, T3out, s);
+    if (T3out) launch_ip_table(xt, nt, d, cb, M, 256, T3out, s);
     hipLaunchKernelGGL(k_coarse_gemm_tiled, dim3((unsigned)ngemm), dim3(256), 0, s, x, xn_buf, nq, d, centT,
                        (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, CoarseT3{});
     return;
@@ -3542,11 +3572,13 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
   const unsigned nqb = nblocks(nq, GQ);
   const int ngemm = (int)(nqb * nblocks(nlist, GC));
   CoarseT3 t3;
-  if (T3out && M > 0 && d % M == 0) {
+  if (T3out && M > 0 && d % M == 0 && nt > 0) {
     t3.out = T3out;
     t3.cb = cb;
     t3.M = M;
-    t3.nblk = (int)(nqb * (unsigned)M);
+    t3.nblk = (int)(nblocks(nt, GQ) * (unsigned)M);
+    t3.x = xt;
+    t3.nq = nt;
   }
   const size_t smem = sizeof(float) * std::max<size_t>((size_t)GQ * ((d + 63) & ~63) + GQ * 9, (size_t)GQ * d);
   if (smem > 64 * 1024) {  // dynamic LDS above 64 KiB is opted into per device

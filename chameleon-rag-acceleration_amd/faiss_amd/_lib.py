@@ -23,7 +23,8 @@ c_i64p = ctypes.POINTER(ctypes.c_int64)
 c_u8p = ctypes.POINTER(ctypes.c_uint8)
 c_handle = ctypes.c_void_p
 
-# name -> (restype, argtypes); mirrors include/ivfpq.h one to one.
+# name -> (restype, argtypes); mirrors include/ivfpq.h one to one, plus the three
+# test hooks of include/ivfpq_test.h (used only by tests/).
 SIGNATURES = {
     "ivfpq_last_error": (ctypes.c_char_p, []),
     "ivfpq_device_count": (ctypes.c_int, []),
@@ -67,6 +68,9 @@ SIGNATURES = {
                                            ctypes.c_int, ctypes.c_int, c_u8p, ctypes.c_int64, c_i64p]),
     "ivfpq_coarse_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p]),
+    "ivfpq_coarse_tables_device": (ctypes.c_int, [c_handle, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.POINTER(ctypes.c_uint64)]),
     "ivfpq_merge_topk_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p]),
@@ -107,7 +111,7 @@ def kernel_source_sha256() -> str:
 def build(force: bool = False) -> str:
     """Compile libivfpq.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
     srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h"))]
-    srcs.append(os.path.join(os.path.dirname(ROOT), "include", "ivfpq.h"))
+    srcs += [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("ivfpq.h", "ivfpq_test.h")]
     stale = not os.path.exists(LIB_PATH) or any(os.path.getmtime(s) > os.path.getmtime(LIB_PATH) for s in srcs)
     if force or stale:
         subprocess.check_call(["make", "-s", "-C", CSRC, "-j4"])

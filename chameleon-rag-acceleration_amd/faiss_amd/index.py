@@ -622,6 +622,30 @@ class IndexIVFPQ:
                                                    ctypes.c_void_p(self._stream(x, stream))))
         return Dq, Iq
 
+    def coarse_tables_device(self, x, x_tables, Iq=None, Dq=None, stream=None):
+        """The list-range shard step's front half on one stream: the coarse quantizer
+        of this rank's queries ``x`` and T3 of the global batch ``x_tables`` (one
+        launch at nlist < 8192).  Returns (Dq, Iq, token); the token goes to
+        ``search_preassigned_device(x_tables, ..., tables=token)``."""
+        import torch
+
+        n = x.shape[0] if x.dim() == 2 else -1
+        self._check_dev(x, "x", torch.float32, (n, self.d))
+        nt = x_tables.shape[0] if x_tables.dim() == 2 else -1
+        self._check_dev(x_tables, "x_tables", torch.float32, (nt, self.d))
+        p = min(self.nprobe, self.nlist)
+        if Iq is None:
+            Iq = torch.empty((n, p), dtype=torch.int64, device=x.device)
+        if Dq is None:
+            Dq = torch.empty((n, p), dtype=torch.float32, device=x.device)
+        self._check_dev(Iq, "Iq", torch.int64, (n, p))
+        self._check_dev(Dq, "Dq", torch.float32, (n, p))
+        tok = ctypes.c_uint64(0)
+        _lib.check(_lib.load().ivfpq_coarse_tables_device(self._h, n, x.data_ptr(), Iq.data_ptr(), Dq.data_ptr(), nt,
+                                                          x_tables.data_ptr(), ctypes.c_void_p(self._stream(x, stream)),
+                                                          ctypes.byref(tok)))
+        return Dq, Iq, tok.value
+
 
 def merge_topk_device(Ds, Is, metric=METRIC_L2, stream=None):
     """Merge S sorted partial results (torch [S, n, k]) into [n, k] on the GPU:

@@ -53,7 +53,7 @@ def balanced_list_ranges(list_sizes, world, code_size=1):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
-def exchange_partials(Dp, Ip, world, group=None):
+def exchange_partials(Dp, Ip, world, group=None, force=False):
     """all_to_all of per-rank partial results.
 
     Dp, Ip: [world * B, k] partial top-k over this rank's lists for the global
@@ -61,7 +61,9 @@ def exchange_partials(Dp, Ip, world, group=None):
     partial for this rank's query slice.  One ``all_to_all_single`` per array:
     row block j of the input (slice j of the batch) goes to rank j, and the
     output's row block s comes from rank s (RCCL over xGMI on GPUs; gloo runs
-    the same call on CPU tensors in the multi-process tests).
+    the same call on CPU tensors in the multi-process tests).  ``force``: run the
+    collective even at world 1 (bench.py --shard-at-1: the RCCL calls and their
+    communicator stream exist as they would at N > 1).
     """
     import torch
     import torch.distributed as dist
@@ -70,7 +72,7 @@ def exchange_partials(Dp, Ip, world, group=None):
     B = n // world
     Ds = torch.empty((world, B, k), dtype=Dp.dtype, device=Dp.device)
     Is = torch.empty((world, B, k), dtype=Ip.dtype, device=Ip.device)
-    if world == 1:
+    if world == 1 and not force:
         Ds[0].copy_(Dp)
         Is[0].copy_(Ip)
         return Ds, Is
@@ -79,13 +81,14 @@ def exchange_partials(Dp, Ip, world, group=None):
     return Ds, Is
 
 
-def all_gather_probes(Dq, Iq, world, group=None):
+def all_gather_probes(Dq, Iq, world, group=None, force=False):
     """All-gather of the per-slice coarse results: [B, nprobe] -> [world * B, nprobe]
-    (slice r from rank r), one ``all_gather_into_tensor`` per array."""
+    (slice r from rank r), one ``all_gather_into_tensor`` per array (``force``: also
+    at world 1, see exchange_partials)."""
     import torch
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not force:
         return Dq, Iq
     outD = torch.empty((world * Dq.shape[0], Dq.shape[1]), dtype=Dq.dtype, device=Dq.device)
     outI = torch.empty((world * Iq.shape[0], Iq.shape[1]), dtype=Iq.dtype, device=Iq.device)

@@ -32,7 +32,10 @@
  * partial list the merge reads is also a set of tagged records (batch epoch +
  * slot): an entry this batch's scan did not leave there is never used -- its probe
  * is rescanned on the device by the merge -- and such events are counted
- * (ivfpq_get_repair_stats; 0 in every real search since the fix).
+ * (ivfpq_get_repair_stats; 0 in every real search since the fix, and the concurrency
+ * gates of the test suite assert it).
+ * Test and diagnostic hooks (fault injection, seeded bounds, workspace dumps) are not part
+ * of this drop-in surface: they are declared in ivfpq_test.h, for the test suite only.
  */
 #ifndef CHAMELEON_IVFPQ_H
 #define CHAMELEON_IVFPQ_H
@@ -155,7 +158,7 @@ int ivfpq_overlap_built(void);
 int ivfpq_get_error_count(ivfpq_index* h, int64_t* out);
 
 /* Stale partial lists (see "Results under concurrent GPU work" above): *stale_reads =
- * (query, merge launch) pairs that read an entry whose tag was not this batch's,
+ * queries (counted once per search) whose merge read an entry whose tag was not this batch's,
  * *repairs = probes the merge rescanned because of one; totals since the handle was
  * created, over all workspaces, after waiting for in-flight searches. */
 int ivfpq_get_repair_stats(ivfpq_index* h, int64_t* stale_reads, int64_t* repairs);
@@ -166,24 +169,18 @@ int ivfpq_get_repair_stats(ivfpq_index* h, int64_t* stale_reads, int64_t* repair
  * 2000; fast path: 1 = fresh at once, 0 = not).  *n_events = events copied to out
  * (out holds max_events x 8 words). */
 int ivfpq_get_repair_log(ivfpq_index* h, uint32_t* out, int max_events, int* n_events);
-/* Test hook for the repair path: every > 0 makes the list scan of later searches skip
- * the stores of the partial lists whose slot (pair * 4 + wave) % every == 1, as if
- * they were lost; 0 (default) turns it off.  Results must stay exact. */
-int ivfpq_set_fault_injection(ivfpq_index* h, int every);
-/* Diagnostics: copy (up to cap bytes of) one per-batch buffer of workspace ws (0..2) as the
- * last search on it left it -- what: 0 partial-list records, 1 partial-list counts, 2 probe
- * masks, 3 tau words, 4 header words, 5 coarse lists, 6 coarse dis0; 7 / 8: the epoch of the
- * last batch planned there / the stream it ran on (8 bytes each); *bytes = its size. */
-int ivfpq_debug_workspace(ivfpq_index* h, int ws, int what, void* dst, int64_t cap, int64_t* bytes);
-/* Test hook for the cross-workgroup bound: the next device search (of exactly n queries)
- * starts with query i's shared bound tau_i = keys[i] instead of +inf (one-shot).  Any
- * keys[i] >= that query's true k-th key is a valid bound, and results must not change. */
-int ivfpq_debug_seed_tau(ivfpq_index* h, int64_t n, const float* keys);
-
 /* Stage entry points of the same search (for per-stage timing): the coarse quantizer
  * (IndexFlatL2::search as in ralm/index_scanner/index_scanner.py:61-77) writing
  * Iq [n][nprobe] / Dq [n][nprobe]; and the per-query inner-product table T3. */
 int ivfpq_coarse_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, float* Dq, void* stream);
+/* The front half of one list-range shard step (the IndexShards step it replaces:
+ * bench_gpu_1bn.py:605-616), on ONE stream: the coarse quantizer of this rank's n queries
+ * x (-> Iq, Dq as ivfpq_coarse_device) and T3 of the n_tables queries x_tables of the
+ * global batch (the table workgroups ride in the same launch as the key tiles at
+ * nlist < 8192).  *token receives the tables for ivfpq_search_preassigned_tables_device
+ * of exactly x_tables (same rules as ivfpq_precompute_tables_device); no side stream. */
+int ivfpq_coarse_tables_device(ivfpq_index* h, int64_t n, const float* x, int64_t* Iq, float* Dq, int64_t n_tables,
+                               const float* x_tables, void* stream, uint64_t* token);
 
 /* Merge S sorted partial results [S][n][k] into [n][k] on the device (the IndexShards
  * merge, bench_gpu_1bn.py:605-616; host argsort merge, bench_multi_cpu_performance_OSDI.py:203-218).

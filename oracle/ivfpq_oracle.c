@@ -249,6 +249,8 @@ void or_precompute_T1(const float *cent, int nlist, int d, const float *codebook
             const float *cw = codebook + ((int64_t)m * ksub + j) * dsub;
             rn[m * ksub + j] = or_tree(cw, cw, dsub, OR_NORM);
         }
+    /* lists are independent (a nlist = 262144 table is 4 GB): one thread per list range */
+#pragma omp parallel for schedule(static)
     for (int l = 0; l < nlist; l++)
         for (int m = 0; m < M; m++)
             for (int j = 0; j < ksub; j++) {

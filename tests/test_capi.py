@@ -9,11 +9,13 @@ import pytest
 import faiss_amd as faiss
 from faiss_amd import _lib
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "ivfpq.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADER = os.path.join(INCLUDE, "ivfpq.h")
+TEST_HEADER = os.path.join(INCLUDE, "ivfpq_test.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(ivfpq_[a-z0-9_]+)\s*\(", src)))
 
@@ -21,10 +23,19 @@ def declared_functions():
 def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     names = declared_functions()
+    hooks = declared_functions(TEST_HEADER)
     assert len(names) >= 30
-    for n in names:
+    for n in names + hooks:
         assert hasattr(lib, n), n
-    assert sorted(_lib.SIGNATURES) == names
+    assert sorted(_lib.SIGNATURES) == sorted(names + hooks)
+
+
+def test_test_hooks_are_not_in_the_drop_in_header():
+    """Fault injection, seeded bounds and workspace dumps are test hooks (ivfpq_test.h),
+    not part of the Faiss-replacing boundary."""
+    hooks = declared_functions(TEST_HEADER)
+    assert sorted(hooks) == ["ivfpq_debug_seed_tau", "ivfpq_debug_workspace", "ivfpq_set_fault_injection"]
+    assert not set(hooks) & set(declared_functions())
 
 
 def test_library_is_gfx950_code_object():

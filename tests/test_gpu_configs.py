@@ -205,14 +205,35 @@ def test_c4_shape_m48_nlist65536(c4_shape, k):
     assert_same(D, I, Dr, Ir)
 
 
-@pytest.mark.parametrize("nshards", [2, 4])
-def test_sliced_coarse_allgather_shards_c2(sift1m, nshards):
+def shard_front(shards, xd, B, tables, check=True):
+    """Rank r's front half of bench.py's shard step: the coarse quantizer of its own
+    slice (with ``tables``: and T3 of the whole batch in the same launch,
+    coarse_tables_device), the probes concatenated (the all_gather), and every rank's
+    preassigned scan of the whole batch (consuming its tables token)."""
+    import torch
+
+    N = len(shards)
+    if tables:
+        fr = [shards[r].coarse_tables_device(xd[r * B:(r + 1) * B], xd) for r in range(N)]
+        for r in ((0, N - 1) if check else ()):  # the coarse half equals the plain coarse step
+            Dc, Ic = shards[r].coarse_device(xd[r * B:(r + 1) * B])
+            assert torch.equal(Ic, fr[r][1]) and torch.equal(Dc, fr[r][0])
+    else:
+        fr = [shards[r].coarse_device(xd[r * B:(r + 1) * B]) + (None,) for r in range(N)]
+    Dq = torch.cat([f[0] for f in fr])
+    Iq = torch.cat([f[1] for f in fr])
+    return Dq, Iq, [f[2] for f in fr]
+
+
+@pytest.mark.parametrize("nshards,tables", [(2, False), (2, True), (4, True)])
+def test_sliced_coarse_allgather_shards_c2(sift1m, nshards, tables):
     """bench.py's shard flow emulated on one GPU: rank r runs the coarse
-    quantizer on its own 1024/N-query slice only, the (list, dis0) arrays of all
-    slices are concatenated (the all_gather), every rank scans its list range
-    for the whole batch with search_preassigned_device, and each slice's N
-    partials are merged on the device (the all_to_all + merge).  Must equal the
-    unsharded oracle bit for bit."""
+    quantizer on its own 1024/N-query slice only (tables: with T3 of the whole
+    batch in the same launch), the (list, dis0) arrays of all slices are
+    concatenated (the all_gather), every rank scans its list range for the whole
+    batch with search_preassigned_device, and each slice's N partials are merged
+    on the device (the all_to_all + merge).  Must equal the unsharded oracle bit
+    for bit."""
     import torch
 
     ix, ox, xq = sift1m
@@ -233,10 +254,8 @@ def test_sliced_coarse_allgather_shards_c2(sift1m, nshards):
                           np.concatenate([ix.invlists.get_ids(l) for l in lists]))
         sh.nprobe = 16
         shards.append(sh)
-    probes = [shards[r].coarse_device(xd[r * B:(r + 1) * B]) for r in range(nshards)]
-    Dq = torch.cat([p[0] for p in probes])
-    Iq = torch.cat([p[1] for p in probes])
-    parts = [sh.search_preassigned_device(xd, 10, Iq, Dq) for sh in shards]
+    Dq, Iq, toks = shard_front(shards, xd, B, tables)
+    parts = [sh.search_preassigned_device(xd, 10, Iq, Dq, tables=t) for sh, t in zip(shards, toks)]
     Dm, Im = [], []
     for r in range(nshards):  # slice r's partials from every rank, merged
         Ds = torch.stack([p[0][r * B:(r + 1) * B] for p in parts])
@@ -333,10 +352,8 @@ def test_c4_shape_eight_list_range_shards(c4_shape, k):
                               np.concatenate([ix.invlists.get_ids(l) for l in lists]))
         sh.nprobe = 32
         shards.append(sh)
-    probes = [shards[r].coarse_device(xd[r * B:(r + 1) * B]) for r in range(N)]
-    Dq = torch.cat([p[0] for p in probes])
-    Iq = torch.cat([p[1] for p in probes])
-    parts = [sh.search_preassigned_device(xd, k, Iq, Dq) for sh in shards]
+    Dq, Iq, toks = shard_front(shards, xd, B, tables=k == 10)  # (the segmented coarse launch + its T3 launch)
+    parts = [sh.search_preassigned_device(xd, k, Iq, Dq, tables=t) for sh, t in zip(shards, toks)]
     Dm, Im = [], []
     for r in range(N):
         D, I = faiss.merge_topk_device(torch.stack([p[0][r * B:(r + 1) * B] for p in parts]),
@@ -440,3 +457,64 @@ def test_precomputed_tables_with_batches_in_flight(sift1m, inflight):
     for s, (D, I) in enumerate(outs):
         assert_same(D.cpu().numpy(), I.cpu().numpy(), *ref[s % 4])
     assert ix.error_count() == 0
+
+
+def test_shard_step_pipelined_on_two_streams(sift1m):
+    """bench.py's shard loop on one GPU, as its ranks issue it at N = 2: per step
+    on stream s % 2, the previous batch of that stream is exchanged and merged
+    first, then this batch's front half (coarse of the own slice + T3 of the
+    global batch in one launch, probes concatenated, preassigned scans consuming
+    the tables token) -- no side stream, no host synchronisation, batches in
+    flight.  Every merged batch equals the unsharded oracle."""
+    import torch
+
+    ix, ox, xq = sift1m
+    ix.nprobe = ox.nprobe = 16
+    N, Bg = 2, 512
+    sizes = ix.invlists.list_sizes()
+    shards = []
+    for lo, hi in balanced_list_ranges(sizes, N, ix.M):
+        sh = faiss.IndexIVFPQ(None, ix.d, ix.nlist, ix.M, 8, device=0)
+        sh.set_trained(ix.centroids(), ix.codebook())
+        sh.set_list_range(lo, hi)
+        lists = [l for l in range(lo, hi) if sizes[l]]
+        sh.add_preencoded(np.concatenate([np.full(sizes[l], l, np.int64) for l in lists]),
+                          np.concatenate([ix.invlists.get_codes(l).reshape(-1, ix.M) for l in lists]),
+                          np.concatenate([ix.invlists.get_ids(l) for l in lists]))
+        sh.nprobe = 16
+        sh.inflight = True
+        shards.append(sh)
+    xs = [torch.from_numpy(xq[i * Bg:(i + 1) * Bg]).cuda() for i in range(2)]
+    B = Bg // N
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    pend, merged = [None, None], []
+
+    def back(j):
+        b, parts = pend[j]
+        pend[j] = None
+        with torch.cuda.stream(streams[j]):
+            for r in range(N):
+                merged.append((b, r, faiss.merge_topk_device(
+                    torch.stack([p[0][r * B:(r + 1) * B] for p in parts]),
+                    torch.stack([p[1][r * B:(r + 1) * B] for p in parts]))))
+
+    torch.cuda.synchronize()
+    for s in range(8):
+        j = s % 2
+        if pend[j] is not None:
+            back(j)
+        x = xs[s % 2]
+        with torch.cuda.stream(streams[j]):
+            Dq, Iq, toks = shard_front(shards, x, B, tables=True, check=False)
+            parts = [sh.search_preassigned_device(x, 10, Iq, Dq, tables=t) for sh, t in zip(shards, toks)]
+        pend[j] = (s % 2, parts)
+    for j in range(2):
+        if pend[j] is not None:
+            back(j)
+    torch.cuda.synchronize()
+    ref = [ox.search(xq[i * Bg:(i + 1) * Bg], 10) for i in range(2)]
+    assert len(merged) == 8 * N
+    for b, r, (D, I) in merged:
+        assert_same(D.cpu().numpy(), I.cpu().numpy(), ref[b][0][r * B:(r + 1) * B], ref[b][1][r * B:(r + 1) * B])
+    for sh in shards:
+        assert sh.error_count() == 0 and sh.repair_stats() == (0, 0)

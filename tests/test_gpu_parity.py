@@ -341,6 +341,7 @@ def test_batches_in_flight_stress(rr_index, k, nst):
         ref.append((D.cpu().numpy(), I.cpu().numpy()))
     streams = [torch.cuda.Stream() for _ in range(nst)]
     e0 = ix.error_count()
+    rs0 = ix.repair_stats()
     bad = []
     for rnd in range(40):
         outs = [(torch.empty((256, k), device="cuda"), torch.empty((256, k), dtype=torch.int64, device="cuda"))
@@ -359,6 +360,11 @@ def test_batches_in_flight_stress(rr_index, k, nst):
                 bad.append((rnd, b))
     assert not bad, f"{len(bad)} of {40 * nb} batches differ: {bad[:8]}"
     assert ix.error_count() == e0
+    # the merge repairs a stale partial list silently (results stay exact), so the
+    # gate also requires that no repair happened: a stale read is a regression
+    rs = ix.repair_stats()
+    assert rs == rs0, f"stale reads / repairs during the stress: {rs[0] - rs0[0]} / {rs[1] - rs0[1]}, " \
+                      f"log {ix.repair_log(8)}"
 
 
 def test_device_entry_points_reject_bad_tensors(golden_dir):
