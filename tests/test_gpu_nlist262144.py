@@ -73,7 +73,7 @@ def test_t1_and_lists(opq_ivf262144):
     assert sizes.shape == (NLIST,) and int(sizes.sum()) == xb.shape[0]
     assert (sizes > 0).sum() > NLIST // 2  # lists past 65 536 are populated too
     assert sizes[200_000:].sum() > 0
-    T1 = ivf.precomputed_table().reshape(NLIST, M, 256)
+    T1 = ivf.precomputed_table.reshape(NLIST, M, 256)
     for l in (0, 131_071, 200_000, NLIST - 1):
         np.testing.assert_array_equal(T1[l], ox.T1.reshape(NLIST, M, 256)[l])
     lists, codes, ids = ivf.invlists.export()
