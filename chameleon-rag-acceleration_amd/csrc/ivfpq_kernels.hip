@@ -2511,6 +2511,272 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   }
 }
 
+// ------------------------------------------------ lean list scan (k <= 16)
+// k_scan_lean: the C2 configuration (G = 4 pairs per item, k <= 16, M <= 16,
+// fused planning) without the candidate queue.  Same items, LUT build, gathers,
+// bounds and partial lists as k_scan_lists<M, 4, 1, JB, true> -- so the same
+// merge and bit-identical results -- but a candidate (a code whose key passes
+// its pair's bound, about 3 per wave and item at C2) is inserted at once into
+// its pair's 16-lane row of the row-packed top-k: one 64-bit compare, a ballot,
+// a DPP row shift and two selects, instead of LDS queue slots from a prefix sum,
+// a queue round trip and a 16-lane sort network per drain.  The bounds tighten
+// at every insertion, and the item's bounds are published (LDS, tau_q) once per
+// super-batch.  The next item's record is unpacked before the item's partial
+// lists are stored and its bounds published, so its wait does not include them.
+__device__ __forceinline__ uint64_t row_shr1_u64(uint64_t v) {  // lane i <- lane i - 1 inside each row of 16
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v, 0x111, 0xf, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(v >> 32), (int)(uint32_t)(v >> 32), 0x111, 0xf, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int M, int JB>
+__global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
+  constexpr int G = 4;
+  constexpr int LUTN = M * 256;
+  constexpr int NV = LUTN / 4 / 256;  // float4 per thread per table row
+  static_assert(NV <= 4 && JB % 2 == 0, "lean scan: M <= 16");
+  __shared__ __attribute__((aligned(16))) float4 lut[LUTN];  // [m][j][g]
+  __shared__ int s_next;
+  __shared__ int32_t s_wb[G];
+  __shared__ int s_ws[8];
+  __shared__ uint16_t s_ex[2][kFusedPlanLists + 1];
+  __shared__ uint16_t s_ord[kFusedPlanLists];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform: positions and slots stay scalar)
+  const int k = a.k;
+  const int ip = a.ip;
+  const int nloc = a.list_hi - a.list_lo;
+  const float inv_np = 1.0f / (float)a.nprobe;
+  const int rg = lane >> 4, re = lane & 15;  // row-packed top-k: lane 16 g + e = entry e of pair g
+  const int2 nn = fused_plan_prefix(pl, nloc, G, s_ex[0], s_ex[1], s_ord, s_ws);
+  const int n_items0 = nn.x, n_items = nn.x + nn.y;
+
+  Item<G> it;
+  auto unpack = [&](const Rec& rc) __attribute__((always_inline)) {
+    const int rv = rc.raw;
+    it.l = rc.l;
+    it.kind = rc.kind;
+    it.cnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - rc.t * G);
+    it.n = __builtin_amdgcn_readlane(rv, 2) - __builtin_amdgcn_readlane(rv, 3);
+    it.beg = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 4) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane(rv, 3));
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      it.pair[g] = __builtin_amdgcn_readlane(rv, 5 + g);
+      it.d0[g] = __int_as_float(__builtin_amdgcn_readlane(rv, 9 + g));
+    }
+    bool bad = false;  // a pair id outside the batch: counted in pl.err, the item scans nothing
+#pragma unroll
+    for (int g = 0; g < G; g++) bad = bad || (g < it.cnt && (unsigned)it.pair[g] >= (unsigned)(a.nq * a.nprobe));
+    if (bad) {
+      if (lane == 0) atomicAdd(pl.err, 1);
+      it.cnt = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) it.pair[g] = 0;
+    }
+#pragma unroll
+    for (int g = 0; g < G; g++) it.q[g] = div_small((g < it.cnt ? it.pair[g] : it.pair[0]), a.nprobe, inv_np);
+  };
+  auto fetch_rec = [&](int idx) __attribute__((always_inline)) {
+    return fused_record(a, pl, nloc, idx, n_items0, s_ex[0], s_ex[1], s_ord, G, lane);
+  };
+
+  if (tid == 0) {
+    const int t = atomicAdd(pl.hdr + 2, 1);
+    s_next = t < n_items ? t : -1;
+  }
+  __syncthreads();
+  int cur = s_next;
+  if (cur >= 0) unpack(fetch_rec(cur));
+  CodeWords<M> cw[JB];
+  while (cur >= 0) {
+    __syncthreads();  // (A) every wave is done with the previous LUT and has read s_next
+    DIAG(0, __builtin_amdgcn_s_memtime());
+    int tnext;
+    if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);
+    int tq[G];
+#pragma unroll
+    for (int g = 0; g < G; g++) tq[g] = tau_get(pl, it.q[g]);
+    // table rows: T1[l] (IP: a T3 row, ignored) and the G pairs' T3 rows, one round trip
+    float4 b1[NV], b3[NV][G];
+    {
+      const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)it.q[0] * LUTN
+                                                             : a.T1 + (int64_t)it.l * LUTN);
+#pragma unroll
+      for (int e = 0; e < NV; e++) {
+        const int v = e * 256 + tid;
+        b1[e] = T1l[v];
+#pragma unroll
+        for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN)[v];
+      }
+    }
+    const int n = it.n;
+    const uint8_t* lc = a.codes + it.beg * M;
+#pragma unroll
+    for (int j = 0; j < JB; j++) {  // the item's first JB x 256 codes, in flight during the LUT stores
+      const int i = j * 256 + wave * 64 + lane;
+      cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
+    }
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+      const int v = e * 256 + tid;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        float4 o;
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          const float x3 = comp(b3[e][g], c);
+          setc(o, g, ip ? -x3 : __builtin_fmaf(x3, -2.0f, comp(b1[e], c)));  // (oracle: one rounding)
+        }
+        lut[4 * v + c] = o;
+      }
+    }
+    if (tid == 0) s_next = tnext < n_items ? tnext : -1;
+    if (tid < G) s_wb[tid] = f2ord(kInf);
+    __syncthreads();  // (B) the LUT, s_next and s_wb are visible
+    DIAG(1, __builtin_amdgcn_s_memtime());
+    const int nxt = s_next;
+    const Rec nrec = fetch_rec(nxt >= 0 ? nxt : cur);  // in flight during the scan
+    int qix[G];
+    float bound[G];
+    bool loose = false;
+    uint64_t rtp[G];  // pair g's k-th word (kKcNone until k entries)
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+      qix[g] = it.q[g];
+      bound[g] = g < it.cnt ? ord2f(tq[g]) : -kInf;
+      loose = loose || bound[g] == kInf;
+      rtp[g] = kKcNone;
+    }
+    uint64_t rk = kKcNone;  // row g: pair g's sorted top-16 (key, position) words
+    uint32_t pub = 0;       // pairs whose k-th word fell since their bound was last published
+
+    // insert candidate (key, position) into pair g's row
+    auto insert = [&](int g, float key, uint32_t pos) __attribute__((always_inline)) {
+      const uint64_t v = pack_kc(key, (int)pos);
+      if (!(v < rtp[g])) return;
+      const uint64_t lt = __builtin_amdgcn_ballot_w64(rk < v);
+      const int p = __popcll((lt >> (16 * g)) & 0xFFFFull);
+      const uint64_t sh = row_shr1_u64(rk);
+      rk = rg == g ? (re > p ? sh : (re == p ? v : rk)) : rk;
+      rtp[g] = readlane_u64(rk, 16 * g + k - 1);
+      if (rtp[g] != kKcNone) bound[g] = fminf(bound[g], kc_key(rtp[g]));
+      pub |= 1u << g;
+    };
+    auto publish = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if (((pub >> g) & 1u) && rtp[g] != kKcNone && lane == 0) {
+          atomicMin(&s_wb[g], f2ord(kc_key(rtp[g])));
+          tau_lower(pl, qix[g], f2ord(kc_key(rtp[g])));
+        }
+      }
+      pub = 0;
+    };
+
+    for (int sb = 0; sb < n; sb += 256 * JB) {
+      if (sb > 0) {
+#pragma unroll
+        for (int j = 0; j < JB; j++) {
+          const int i = sb + j * 256 + wave * 64 + lane;
+          cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
+        }
+      }
+      const int tn = min(JB, (n - sb + 255) >> 8);  // chunks with codes (wave-uniform)
+      const bool last_sb = sb + 256 * JB >= n;
+      // G keys per code: dis0 + sum_m LUT[m][code_m], sequential in m (the oracle's order)
+      float dis[JB][G];
+#pragma unroll
+      for (int jd = 0; jd < JB / 2; jd++) {
+        if (2 * jd < tn) {
+          CodeWords<M> cc[2] = {cw[2 * jd], cw[2 * jd + 1]};
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(cc[h].w[v]));
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int g = 0; g < G; g++) dis[2 * jd + h][g] = it.d0[g];
+#pragma unroll
+          for (int m = 0; m < M; m++) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+              const float4 v = lut[m * 256 + cc[h].byte(m)];
+#pragma unroll
+              for (int g = 0; g < G; g++) dis[2 * jd + h][g] = dis[2 * jd + h][g] + comp(v, g);
+            }
+          }
+        }
+      }
+      DIAG_ONLY(asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1]));)
+      if (loose) {
+        // a pair without a bound gets one from this super-batch: the k-th smallest
+        // of the 64 lane minima bounds the final k-th key (k distinct codes)
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          if (bound[g] != kInf) continue;  // wave-uniform
+          float mn = kInf;
+#pragma unroll
+          for (int j = 0; j < JB; j++)
+            if (j < tn && sb + j * 256 + wave * 64 + lane < n) mn = fminf(mn, dis[j][g]);
+          const float T = wave_kth_smallest(mn, k, lane);
+          if (T < kInf && lane == 0) {
+            atomicMin(&s_wb[g], f2ord(T));
+            tau_lower(pl, qix[g], f2ord(T));
+          }
+        }
+      }
+      loose = false;
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        // (readfirstlane: one value for the wave, DESIGN.md §4 "Uniform bounds")
+        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(__builtin_amdgcn_readfirstlane(s_wb[g])));
+        loose = loose || bound[g] == kInf;
+      }
+      // admission: one ballot per (chunk, pair); each candidate inserted at once
+#pragma unroll
+      for (int j = 0; j < JB; j++) {
+        if (j < tn) {  // wave-uniform
+          const int i0 = sb + j * 256 + wave * 64;
+          const bool valid = i0 + lane < n;
+#pragma unroll
+          for (int g = 0; g < G; g++) {
+            uint64_t mk = __builtin_amdgcn_ballot_w64(valid && dis[j][g] <= bound[g]);
+            while (mk) {
+              const int src = (int)__builtin_ctzll(mk);
+              mk &= mk - 1;
+              insert(g, readlane_f(dis[j][g], src), (uint32_t)(i0 + src));
+            }
+          }
+        }
+      }
+      if (!last_sb) publish();  // (the last super-batch's bounds: after the next record is unpacked)
+    }
+    DIAG(2, __builtin_amdgcn_s_memtime());
+    // the partial lists' store operands, then the next item's fields (its record
+    // load is older than the stores and atomics below, so this waits for it alone)
+    int pr = it.pair[0];
+#pragma unroll
+    for (int g = 1; g < G; g++) pr = rg == g ? it.pair[g] : pr;
+    const int64_t slot = (int64_t)pr * 4 + wave;
+    const bool st = rg < it.cnt && re < k && !(pl.fault > 0 && slot % pl.fault == 1);  // (fault: test hook)
+    const int64_t beg = it.beg;
+    if (nxt >= 0) unpack(nrec);
+    publish();
+    if (st) {
+      const bool empty = rk == kKcNone;
+      pl.part[slot * pl.ks + re] =
+          part_rec(empty ? FLT_MAX : kc_key(rk), part_tag(pl.epoch, slot) | xcc_tag(), empty ? -1 : beg + (int64_t)(uint32_t)rk);
+    }
+    DIAG(3, __builtin_amdgcn_s_memtime());
+    cur = nxt;
+  }
+}
+
 // ------------------------------------------- large-nlist coarse (no key matrix)
 // Segmented coarse quantizer: workgroup = 16 queries x one segment of `seg`
 // centroids, walked in key tiles of 128 (coarse_key_tile: the MFMA keys of
@@ -3773,6 +4039,11 @@ int device_cus() {
   return cus;
 }
 
+#ifndef SCAN_LEAN
+#define SCAN_LEAN 1
+#endif
+constexpr bool kScanLean = SCAN_LEAN != 0;  // (-DSCAN_LEAN=0: the queue-based k_scan_lists for A/B builds)
+
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
@@ -3782,7 +4053,9 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   constexpr int JB = M <= 16 ? 6 : 4;
   if (ev) (void)hipEventRecord(ev[0], s);
   if constexpr (G == 4 && R == 1) {
-    if (a.k <= 16) {  // r03 A/B at C2: 115.1 vs 125.7 us
+    if (a.k <= 16 && pl.fused && kScanLean && M <= 16) {  // (row-packed top-k, insertion instead of a queue)
+      hipLaunchKernelGGL((k_scan_lean<M, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+    } else if (a.k <= 16) {  // r03 A/B at C2: 115.1 vs 125.7 us
       hipLaunchKernelGGL((k_scan_lists<M, G, R, JB, true>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
     } else {
       hipLaunchKernelGGL((k_scan_lists<M, G, R, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
