@@ -604,6 +604,16 @@ __device__ __forceinline__ int tau_get(const ListPlan& pl, int64_t q) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
   return hi == ~pl.epoch ? (int)(lo ^ 0x80000000u) : f2ord(kInf);
 }
+// tau_get in two halves: the agent-scope load (kept in flight as a raw word) and
+// its wave-uniform decode at the use
+__device__ __forceinline__ uint64_t tau_load(const ListPlan& pl, int64_t q) {
+  return __hip_atomic_load(pl.tauq + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int tau_decode(const ListPlan& pl, uint64_t v) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));  // (see tau_get)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  return hi == ~pl.epoch ? (int)(lo ^ 0x80000000u) : f2ord(kInf);
+}
 // tau_q := min(tau_q, o) within this batch (any k real candidates bound the final k-th key)
 __device__ __forceinline__ void tau_lower(const ListPlan& pl, int64_t q, int o) {
   const uint64_t w = ((uint64_t)(~pl.epoch) << 32) | ((uint32_t)o ^ 0x80000000u);
@@ -2511,6 +2521,19 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
   }
 }
 
+#ifndef SCAN_LEAN
+#define SCAN_LEAN 1
+#endif
+#ifndef SCAN_PREFETCH
+#define SCAN_PREFETCH 1
+#endif
+constexpr bool kScanLean = SCAN_LEAN != 0;  // (-DSCAN_LEAN=0: the queue-based k_scan_lists for A/B builds)
+constexpr bool kScanPrefetch = SCAN_PREFETCH != 0;  // (-DSCAN_PREFETCH=0: tables loaded at the item start)
+#ifndef SCAN_LEAN_JB
+#define SCAN_LEAN_JB 4
+#endif
+constexpr int kLeanJB = SCAN_LEAN_JB;  // code chunks per super-batch of k_scan_lean
+
 // ------------------------------------------------ lean list scan (k <= 16)
 // k_scan_lean: the C2 configuration (G = 4 pairs per item, k <= 16, M <= 16,
 // fused planning) without the candidate queue.  Same items, LUT build, gathers,
@@ -2592,27 +2615,34 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
   int cur = s_next;
   if (cur >= 0) unpack(fetch_rec(cur));
   CodeWords<M> cw[JB];
+  // An item's table rows: T1[l] (IP: a T3 row, ignored) and its G pairs' T3 rows,
+  // one round trip, and its queries' bounds tau_q.  With kScanPrefetch they are
+  // loaded for the NEXT item right after the current item's last gathers (its
+  // record has arrived by then), so that the 80 KB per item from L2 / the Infinity
+  // Cache arrive during the admission, the partial writes and the barrier instead
+  // of stalling the next LUT build (the build waited ~5 000 cycles for them, r04
+  // stamps: about the per-CU Infinity-Cache rate).
+  uint64_t tw[G];  // the queries' tau words, decoded after barrier B
+  float4 b1[NV], b3[NV][G];
+  auto prefetch = [&](int l, const int (&q)[G]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < G; g++) tw[g] = tau_load(pl, q[g]);
+    const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)q[0] * LUTN : a.T1 + (int64_t)l * LUTN);
+#pragma unroll
+    for (int e = 0; e < NV; e++) {
+      const int v = e * 256 + tid;
+      b1[e] = T1l[v];
+#pragma unroll
+      for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)q[g] * LUTN)[v];
+    }
+  };
+  if (kScanPrefetch && cur >= 0) prefetch(it.l, it.q);
   while (cur >= 0) {
     __syncthreads();  // (A) every wave is done with the previous LUT and has read s_next
     DIAG(0, __builtin_amdgcn_s_memtime());
     int tnext;
     if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);
-    int tq[G];
-#pragma unroll
-    for (int g = 0; g < G; g++) tq[g] = tau_get(pl, it.q[g]);
-    // table rows: T1[l] (IP: a T3 row, ignored) and the G pairs' T3 rows, one round trip
-    float4 b1[NV], b3[NV][G];
-    {
-      const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)it.q[0] * LUTN
-                                                             : a.T1 + (int64_t)it.l * LUTN);
-#pragma unroll
-      for (int e = 0; e < NV; e++) {
-        const int v = e * 256 + tid;
-        b1[e] = T1l[v];
-#pragma unroll
-        for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)it.q[g] * LUTN)[v];
-      }
-    }
+    if (!kScanPrefetch) prefetch(it.l, it.q);
     const int n = it.n;
     const uint8_t* lc = a.codes + it.beg * M;
 #pragma unroll
@@ -2647,7 +2677,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
       qix[g] = it.q[g];
-      bound[g] = g < it.cnt ? ord2f(tq[g]) : -kInf;
+      bound[g] = g < it.cnt ? ord2f(tau_decode(pl, tw[g])) : -kInf;
       loose = loose || bound[g] == kInf;
       rtp[g] = kKcNone;
     }
@@ -2678,20 +2708,15 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     };
 
     for (int sb = 0; sb < n; sb += 256 * JB) {
-      if (sb > 0) {
-#pragma unroll
-        for (int j = 0; j < JB; j++) {
-          const int i = sb + j * 256 + wave * 64 + lane;
-          cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
-        }
-      }
-      const int tn = min(JB, (n - sb + 255) >> 8);  // chunks with codes (wave-uniform)
+      // this wave's chunks with codes (wave-uniform): chunk j holds codes sb + 256 j + 64 wave + lane
+      const int tn = max(0, min(JB, (n - sb - 64 * wave + 255) >> 8));
       const bool last_sb = sb + 256 * JB >= n;
-      // G keys per code: dis0 + sum_m LUT[m][code_m], sequential in m (the oracle's order)
+      // G keys per code: dis0 + sum_m LUT[m][code_m], sequential in m (the oracle's order);
+      // two chunks at a time (their 2 M gathers interleaved), a lone last chunk alone
       float dis[JB][G];
 #pragma unroll
       for (int jd = 0; jd < JB / 2; jd++) {
-        if (2 * jd < tn) {
+        if (2 * jd + 1 < tn) {
           CodeWords<M> cc[2] = {cw[2 * jd], cw[2 * jd + 1]};
 #pragma unroll
           for (int h = 0; h < 2; h++)
@@ -2710,9 +2735,42 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
               for (int g = 0; g < G; g++) dis[2 * jd + h][g] = dis[2 * jd + h][g] + comp(v, g);
             }
           }
+        } else if (2 * jd < tn) {
+          CodeWords<M> cc = cw[2 * jd];
+#pragma unroll
+          for (int v = 0; v < M / 4; v++) asm volatile("" : "+v"(cc.w[v]));
+#pragma unroll
+          for (int g = 0; g < G; g++) dis[2 * jd][g] = it.d0[g];
+#pragma unroll
+          for (int m = 0; m < M; m++) {
+            const float4 v = lut[m * 256 + cc.byte(m)];
+#pragma unroll
+            for (int g = 0; g < G; g++) dis[2 * jd][g] = dis[2 * jd][g] + comp(v, g);
+          }
         }
       }
       DIAG_ONLY(asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1]));)
+      if (!last_sb) {  // the next super-batch's codes, in flight during this one's admission
+#pragma unroll
+        for (int j = 0; j < JB; j++) {
+          const int i = sb + 256 * JB + j * 256 + wave * 64 + lane;
+          cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
+        }
+      }
+      if (kScanPrefetch && last_sb && nxt >= 0) {  // the next item's tables and bounds (see prefetch; after the codes are dead)
+        const int rv = nrec.raw;
+        const int ncnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - nrec.t * G);
+        const int p0 = __builtin_amdgcn_readlane(rv, 5);
+        int nq[G];
+#pragma unroll
+        for (int g = 0; g < G; g++) {
+          const int pg = g < ncnt ? __builtin_amdgcn_readlane(rv, 5 + g) : p0;
+          // (clamped: a pair id outside the batch is rejected by unpack, but is never an address)
+          nq[g] = min(div_small(pg, a.nprobe, inv_np), (int)a.nq - 1);
+          nq[g] = max(nq[g], 0);
+        }
+        prefetch(nrec.l, nq);
+      }
       if (loose) {
         // a pair without a bound gets one from this super-batch: the k-th smallest
         // of the 64 lane minima bounds the final k-th key (k distinct codes)
@@ -4039,11 +4097,6 @@ int device_cus() {
   return cus;
 }
 
-#ifndef SCAN_LEAN
-#define SCAN_LEAN 1
-#endif
-constexpr bool kScanLean = SCAN_LEAN != 0;  // (-DSCAN_LEAN=0: the queue-based k_scan_lists for A/B builds)
-
 template <int M, int R>
 static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s, hipEvent_t* ev) {
   constexpr int G = scan_group(M, R);
@@ -4054,7 +4107,7 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
   if (ev) (void)hipEventRecord(ev[0], s);
   if constexpr (G == 4 && R == 1) {
     if (a.k <= 16 && pl.fused && kScanLean && M <= 16) {  // (row-packed top-k, insertion instead of a queue)
-      hipLaunchKernelGGL((k_scan_lean<M, JB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
+      hipLaunchKernelGGL((k_scan_lean<M, kLeanJB>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
     } else if (a.k <= 16) {  // r03 A/B at C2: 115.1 vs 125.7 us
       hipLaunchKernelGGL((k_scan_lists<M, G, R, JB, true>), dim3((unsigned)pl.grid), dim3(256), 0, s, a, pl);
     } else {

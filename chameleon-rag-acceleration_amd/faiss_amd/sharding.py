@@ -53,6 +53,19 @@ def balanced_list_ranges(list_sizes, world, code_size=1):
     return [(bounds[r], bounds[r + 1]) for r in range(world)]
 
 
+def _coalesced(group, device):
+    """One RCCL launch for the two collectives of an exchange (distances and labels):
+    torch's coalescing manager around them when the group is an nccl (RCCL) group;
+    a null context otherwise (gloo, the CPU tests)."""
+    import contextlib
+
+    import torch.distributed as dist
+
+    if dist.get_backend(group) != "nccl":
+        return contextlib.nullcontext()
+    return dist.distributed_c10d._coalescing_manager(group=group, device=device)
+
+
 def exchange_partials(Dp, Ip, world, group=None, force=False):
     """all_to_all of per-rank partial results.
 
@@ -76,8 +89,10 @@ def exchange_partials(Dp, Ip, world, group=None, force=False):
         Ds[0].copy_(Dp)
         Is[0].copy_(Ip)
         return Ds, Is
-    dist.all_to_all_single(Ds.view(world * B, k), Dp.contiguous(), group=group)
-    dist.all_to_all_single(Is.view(world * B, k), Ip.contiguous(), group=group)
+    Dp, Ip = Dp.contiguous(), Ip.contiguous()
+    with _coalesced(group, Dp.device):
+        dist.all_to_all_single(Ds.view(world * B, k), Dp, group=group)
+        dist.all_to_all_single(Is.view(world * B, k), Ip, group=group)
     return Ds, Is
 
 
@@ -92,8 +107,10 @@ def all_gather_probes(Dq, Iq, world, group=None, force=False):
         return Dq, Iq
     outD = torch.empty((world * Dq.shape[0], Dq.shape[1]), dtype=Dq.dtype, device=Dq.device)
     outI = torch.empty((world * Iq.shape[0], Iq.shape[1]), dtype=Iq.dtype, device=Iq.device)
-    dist.all_gather_into_tensor(outD, Dq.contiguous(), group=group)
-    dist.all_gather_into_tensor(outI, Iq.contiguous(), group=group)
+    Dq, Iq = Dq.contiguous(), Iq.contiguous()
+    with _coalesced(group, Dq.device):
+        dist.all_gather_into_tensor(outD, Dq, group=group)
+        dist.all_gather_into_tensor(outI, Iq, group=group)
     return outD, outI
 
 
