@@ -403,7 +403,9 @@ def main():
     scan_avg_ms = scan_ms / max(scan_n, 1)
     lists_ms, lists_n = stages["lists"]
     bytes_per_step = sum(bytes_alg[s % args.nbatches] for s in range(args.steps)) / args.steps
-    kernel = f"k_scan_lists<{args.M},...> (list-major LUT + PQ scan + top-k, every probe)"
+    kernel = (f"k_scan_lean<{args.M},...> (list-major LUT + PQ scan + row-packed top-k, every probe)"
+              if k <= 16 and args.M <= 16 else
+              f"k_scan_lists<{args.M},...> (list-major LUT + PQ scan + top-k, every probe)")
     avg_launch_ms = lists_ms / max(lists_n, 1)
     timed = [s for s in range(args.steps) if s % args.event_every == 0]  # the steps with events
     bytes_per_launch = sum(bytes_lists[s % args.nbatches] for s in timed) / len(timed)

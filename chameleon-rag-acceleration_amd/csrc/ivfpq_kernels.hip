@@ -2525,12 +2525,12 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #define SCAN_LEAN 1
 #endif
 #ifndef SCAN_PREFETCH
-#define SCAN_PREFETCH 1
+#define SCAN_PREFETCH 0  // (r06 A/B at C2: 106.9 us with, 106.8 without at JB 4; JB 6 without: 103.7)
 #endif
 constexpr bool kScanLean = SCAN_LEAN != 0;  // (-DSCAN_LEAN=0: the queue-based k_scan_lists for A/B builds)
 constexpr bool kScanPrefetch = SCAN_PREFETCH != 0;  // (-DSCAN_PREFETCH=0: tables loaded at the item start)
 #ifndef SCAN_LEAN_JB
-#define SCAN_LEAN_JB 4
+#define SCAN_LEAN_JB 6
 #endif
 constexpr int kLeanJB = SCAN_LEAN_JB;  // code chunks per super-batch of k_scan_lean
 
@@ -2637,6 +2637,8 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     }
   };
   if (kScanPrefetch && cur >= 0) prefetch(it.l, it.q);
+  int it_no = 0;  // (DIAG stamps)
+  (void)it_no;
   while (cur >= 0) {
     __syncthreads();  // (A) every wave is done with the previous LUT and has read s_next
     DIAG(0, __builtin_amdgcn_s_memtime());
@@ -2683,6 +2685,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     }
     uint64_t rk = kKcNone;  // row g: pair g's sorted top-16 (key, position) words
     uint32_t pub = 0;       // pairs whose k-th word fell since their bound was last published
+    DIAG_ONLY(uint64_t d_gather = 0, d_bounds = 0, d_admit = 0, n_ins = 0;)
 
     // insert candidate (key, position) into pair g's row
     auto insert = [&](int g, float key, uint32_t pos) __attribute__((always_inline)) {
@@ -2695,6 +2698,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
       rtp[g] = readlane_u64(rk, 16 * g + k - 1);
       if (rtp[g] != kKcNone) bound[g] = fminf(bound[g], kc_key(rtp[g]));
       pub |= 1u << g;
+      DIAG_ONLY(n_ins++;)
     };
     auto publish = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -2707,7 +2711,9 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
       pub = 0;
     };
 
+    DIAG(11, __builtin_amdgcn_s_memtime());
     for (int sb = 0; sb < n; sb += 256 * JB) {
+      DIAG_ONLY(const uint64_t tg0 = __builtin_amdgcn_s_memtime();)
       // this wave's chunks with codes (wave-uniform): chunk j holds codes sb + 256 j + 64 wave + lane
       const int tn = max(0, min(JB, (n - sb - 64 * wave + 255) >> 8));
       const bool last_sb = sb + 256 * JB >= n;
@@ -2749,7 +2755,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
           }
         }
       }
-      DIAG_ONLY(asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1]));)
+      DIAG_ONLY(asm volatile("" ::"v"(dis[0][0]), "v"(dis[JB - 1][G - 1])); const uint64_t tg1 = __builtin_amdgcn_s_memtime(); d_gather += tg1 - tg0;)
       if (!last_sb) {  // the next super-batch's codes, in flight during this one's admission
 #pragma unroll
         for (int j = 0; j < JB; j++) {
@@ -2795,6 +2801,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
         if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(__builtin_amdgcn_readfirstlane(s_wb[g])));
         loose = loose || bound[g] == kInf;
       }
+      DIAG_ONLY(const uint64_t tb1 = __builtin_amdgcn_s_memtime(); d_bounds += tb1 - tg1;)
       // admission: one ballot per (chunk, pair); each candidate inserted at once
 #pragma unroll
       for (int j = 0; j < JB; j++) {
@@ -2812,9 +2819,17 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
           }
         }
       }
+      DIAG_ONLY(d_admit += __builtin_amdgcn_s_memtime() - tb1;)
       if (!last_sb) publish();  // (the last super-batch's bounds: after the next record is unpacked)
     }
     DIAG(2, __builtin_amdgcn_s_memtime());
+    DIAG(4, n);
+    DIAG(5, it.cnt | (it.kind << 8));
+    DIAG(6, d_gather);
+    DIAG(7, n_ins);
+    DIAG(8, d_bounds);
+    DIAG(9, d_admit);
+    DIAG(10, 0);
     // the partial lists' store operands, then the next item's fields (its record
     // load is older than the stores and atomics below, so this waits for it alone)
     int pr = it.pair[0];
@@ -2831,6 +2846,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
           part_rec(empty ? FLT_MAX : kc_key(rk), part_tag(pl.epoch, slot) | xcc_tag(), empty ? -1 : beg + (int64_t)(uint32_t)rk);
     }
     DIAG(3, __builtin_amdgcn_s_memtime());
+    DIAG_ONLY(it_no++;)
     cur = nxt;
   }
 }

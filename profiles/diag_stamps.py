@@ -32,10 +32,11 @@ def main():
     from faiss_amd import _lib, datasets
 
     nb = int(os.environ.get("NB", "1000000"))
-    xt = datasets.synthetic_sift_like(100_000, 128, seed=4321)
+    xt = datasets.synthetic_sift_like(100_000, 128, seed=4321)  # (bench.py's data: 200k centres)
     xb = datasets.synthetic_sift_like(nb, 128, seed=1234)
     xq = datasets.synthetic_sift_like(1024, 128, seed=123)
     ix = faiss.index_factory(128, "IVF1024,PQ16")
+    ix.niter_coarse = ix.niter_pq = 25
     ix.train(xt)
     ix.add(xb)
     ix.nprobe = 16

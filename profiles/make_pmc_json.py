@@ -52,7 +52,7 @@ def main(d, key, out, lib=None):
     # the bench's own scan kernel: of the list-scan instantiations, the most launched
     # (the bench's k = 100 extra runs another one a few times)
     nlaunch = {k: len(agg.get((k, "FETCH_SIZE"), [])) for k in kernels}
-    lists = sorted((k for k in kernels if k.startswith(("k_scan_pipe", "k_scan_lists"))), key=lambda k: -nlaunch[k])
+    lists = sorted((k for k in kernels if k.startswith(("k_scan_lean", "k_scan_pipe", "k_scan_lists"))), key=lambda k: -nlaunch[k])
     topk = [k for k in kernels if k.startswith("k_scan_topk") and "true" not in k]
     main_k = (lists or topk or [None])[0]
     res["kernel"] = main_k

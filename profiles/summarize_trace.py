@@ -33,7 +33,7 @@ def main(path, steps, passes=None):
         print(f"{n[:48]:48s} {len(v):6d} {sum(v)/len(v):9.2f} {min(v):9.2f} {sum(v):10.1f}")
     if passes:
         w, k = passes
-        scans = [n for n in agg if "k_scan_lists<16, 4, 1" in n]
+        scans = [n for n in agg if "k_scan_lists<16, 4, 1" in n or "k_scan_lean<16" in n]
         if scans:
             name = scans[0]
             rs = [r for r in tail if short(r["Kernel_Name"]) == name]
