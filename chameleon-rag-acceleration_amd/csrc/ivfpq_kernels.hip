@@ -2546,6 +2546,13 @@ constexpr int kLeanJB = SCAN_LEAN_JB;  // code chunks per super-batch of k_scan_
 // at every insertion, and the item's bounds are published (LDS, tau_q) once per
 // super-batch.  The next item's record is unpacked before the item's partial
 // lists are stored and its bounds published, so its wait does not include them.
+// pack_kc of a key given by its bits, in integer ops (scalar when b is):
+// unsigned order of the high word == float order, -0 folded into +0
+__device__ __forceinline__ uint64_t pack_kc_bits(uint32_t b, uint32_t pos) {
+  b = b == 0x80000000u ? 0u : b;
+  const uint32_t o = (int32_t)b >= 0 ? (b ^ 0x80000000u) : ~b;
+  return ((uint64_t)o << 32) | pos;
+}
 __device__ __forceinline__ uint64_t row_shr1_u64(uint64_t v) {  // lane i <- lane i - 1 inside each row of 16
   const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v, 0x111, 0xf, 0xf, false);
   const uint32_t hi =
@@ -2624,19 +2631,24 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
   // stamps: about the per-CU Infinity-Cache rate).
   uint64_t tw[G];  // the queries' tau words, decoded after barrier B
   float4 b1[NV], b3[NV][G];
-  auto prefetch = [&](int l, const int (&q)[G]) __attribute__((always_inline)) {
+  // (with kScanPrefetch the T3 rows, 64 of the 80 KB, come ahead; the T1 row is
+  // loaded at the item start: all 80 KB ahead left too few VGPRs at JB 6)
+  auto prefetch_t3 = [&](const int (&q)[G]) __attribute__((always_inline)) {
 #pragma unroll
     for (int g = 0; g < G; g++) tw[g] = tau_load(pl, q[g]);
-    const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)q[0] * LUTN : a.T1 + (int64_t)l * LUTN);
 #pragma unroll
     for (int e = 0; e < NV; e++) {
       const int v = e * 256 + tid;
-      b1[e] = T1l[v];
 #pragma unroll
       for (int g = 0; g < G; g++) b3[e][g] = reinterpret_cast<const float4*>(a.T3 + (int64_t)q[g] * LUTN)[v];
     }
   };
-  if (kScanPrefetch && cur >= 0) prefetch(it.l, it.q);
+  auto load_t1 = [&](int l, int q0) __attribute__((always_inline)) {
+    const float4* T1l = reinterpret_cast<const float4*>(ip ? a.T3 + (int64_t)q0 * LUTN : a.T1 + (int64_t)l * LUTN);
+#pragma unroll
+    for (int e = 0; e < NV; e++) b1[e] = T1l[e * 256 + tid];
+  };
+  if (kScanPrefetch && cur >= 0) prefetch_t3(it.q);
   int it_no = 0;  // (DIAG stamps)
   (void)it_no;
   while (cur >= 0) {
@@ -2644,7 +2656,8 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     DIAG(0, __builtin_amdgcn_s_memtime());
     int tnext;
     if (tid == 0) tnext = atomicAdd(pl.hdr + 2, 1);
-    if (!kScanPrefetch) prefetch(it.l, it.q);
+    if (!kScanPrefetch) prefetch_t3(it.q);
+    load_t1(it.l, it.q[0]);
     const int n = it.n;
     const uint8_t* lc = a.codes + it.beg * M;
 #pragma unroll
@@ -2672,6 +2685,14 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     DIAG(1, __builtin_amdgcn_s_memtime());
     const int nxt = s_next;
     const Rec nrec = fetch_rec(nxt >= 0 ? nxt : cur);  // in flight during the scan
+    // this item's fields the scan still needs after the next record is unpacked into `it`
+    const int cnt = it.cnt;
+    int pr = it.pair[0];  // the partial-list slot of this lane's row (pair rg, this wave)
+#pragma unroll
+    for (int g = 1; g < G; g++) pr = rg == g ? it.pair[g] : pr;
+    const int64_t slot = (int64_t)pr * 4 + wave;
+    const bool st = rg < cnt && re < k && !(pl.fault > 0 && slot % pl.fault == 1);  // (fault: test hook)
+    const int64_t beg = it.beg;
     int qix[G];
     float bound[G];
     bool loose = false;
@@ -2679,7 +2700,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
 #pragma unroll
     for (int g = 0; g < G; g++) {
       qix[g] = it.q[g];
-      bound[g] = g < it.cnt ? ord2f(tau_decode(pl, tw[g])) : -kInf;
+      bound[g] = g < cnt ? ord2f(tau_decode(pl, tw[g])) : -kInf;
       loose = loose || bound[g] == kInf;
       rtp[g] = kKcNone;
     }
@@ -2688,17 +2709,30 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     DIAG_ONLY(uint64_t d_gather = 0, d_bounds = 0, d_admit = 0, n_ins = 0;)
 
     // insert candidate (key, position) into pair g's row
-    auto insert = [&](int g, float key, uint32_t pos) __attribute__((always_inline)) {
-      const uint64_t v = pack_kc(key, (int)pos);
-      if (!(v < rtp[g])) return;
+    // Insert candidate word v into pair g's row.  The row keeps its 16 smallest
+    // words; a word that lands past the k-th is harmless (it is never published),
+    // so pair g's k-th word and bound are refreshed once per super-batch (refresh),
+    // not per insertion: one ballot, a DPP row shift and selects, no readlane chain.
+    uint32_t ins = 0;  // pairs with an insertion since the last refresh
+    auto insert = [&](int g, uint64_t v) __attribute__((always_inline)) {
+      if (!(v < rtp[g])) return;  // (rtp[g]: pair g's k-th word at the last refresh)
       const uint64_t lt = __builtin_amdgcn_ballot_w64(rk < v);
       const int p = __popcll((lt >> (16 * g)) & 0xFFFFull);
       const uint64_t sh = row_shr1_u64(rk);
       rk = rg == g ? (re > p ? sh : (re == p ? v : rk)) : rk;
-      rtp[g] = readlane_u64(rk, 16 * g + k - 1);
-      if (rtp[g] != kKcNone) bound[g] = fminf(bound[g], kc_key(rtp[g]));
-      pub |= 1u << g;
+      ins |= 1u << g;
       DIAG_ONLY(n_ins++;)
+    };
+    auto refresh = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        if ((ins >> g) & 1u) {
+          rtp[g] = readlane_u64(rk, 16 * g + k - 1);
+          if (rtp[g] != kKcNone) bound[g] = fminf(bound[g], kc_key(rtp[g]));
+        }
+      }
+      pub |= ins;
+      ins = 0;
     };
     auto publish = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -2763,19 +2797,12 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
           cw[j].load(lc + (int64_t)(i < n ? i : 0) * M);
         }
       }
-      if (kScanPrefetch && last_sb && nxt >= 0) {  // the next item's tables and bounds (see prefetch; after the codes are dead)
-        const int rv = nrec.raw;
-        const int ncnt = min(G, min(__builtin_amdgcn_readlane(rv, 1), pl.cap) - nrec.t * G);
-        const int p0 = __builtin_amdgcn_readlane(rv, 5);
-        int nq[G];
-#pragma unroll
-        for (int g = 0; g < G; g++) {
-          const int pg = g < ncnt ? __builtin_amdgcn_readlane(rv, 5 + g) : p0;
-          // (clamped: a pair id outside the batch is rejected by unpack, but is never an address)
-          nq[g] = min(div_small(pg, a.nprobe, inv_np), (int)a.nq - 1);
-          nq[g] = max(nq[g], 0);
-        }
-        prefetch(nrec.l, nq);
+      if (kScanPrefetch && last_sb && nxt >= 0) {
+        // the next item: its record unpacked here (its load is the oldest in flight, so
+        // this waits for nothing younger), then its table rows and bounds loaded, in
+        // flight during this item's admission, partial writes and barrier (see prefetch)
+        unpack(nrec);
+        prefetch_t3(it.q);
       }
       if (loose) {
         // a pair without a bound gets one from this super-batch: the k-th smallest
@@ -2798,27 +2825,34 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
 #pragma unroll
       for (int g = 0; g < G; g++) {
         // (readfirstlane: one value for the wave, DESIGN.md §4 "Uniform bounds")
-        if (g < it.cnt) bound[g] = fminf(bound[g], ord2f(__builtin_amdgcn_readfirstlane(s_wb[g])));
+        if (g < cnt) bound[g] = fminf(bound[g], ord2f(__builtin_amdgcn_readfirstlane(s_wb[g])));
         loose = loose || bound[g] == kInf;
       }
       DIAG_ONLY(const uint64_t tb1 = __builtin_amdgcn_s_memtime(); d_bounds += tb1 - tg1;)
-      // admission: one ballot per (chunk, pair); each candidate inserted at once
+      // admission: one ballot per chunk for all pairs, then per pair only where a
+      // chunk has candidates; each candidate inserted at once
 #pragma unroll
       for (int j = 0; j < JB; j++) {
         if (j < tn) {  // wave-uniform
           const int i0 = sb + j * 256 + wave * 64;
           const bool valid = i0 + lane < n;
+          bool c = false;
+#pragma unroll
+          for (int g = 0; g < G; g++) c = c || dis[j][g] <= bound[g];
+          if (__builtin_amdgcn_ballot_w64(valid && c) == 0) continue;
 #pragma unroll
           for (int g = 0; g < G; g++) {
             uint64_t mk = __builtin_amdgcn_ballot_w64(valid && dis[j][g] <= bound[g]);
             while (mk) {
               const int src = (int)__builtin_ctzll(mk);
               mk &= mk - 1;
-              insert(g, readlane_f(dis[j][g], src), (uint32_t)(i0 + src));
+              const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(dis[j][g]), src);
+              insert(g, pack_kc_bits(b, (uint32_t)(i0 + src)));
             }
           }
         }
       }
+      refresh();
       DIAG_ONLY(d_admit += __builtin_amdgcn_s_memtime() - tb1;)
       if (!last_sb) publish();  // (the last super-batch's bounds: after the next record is unpacked)
     }
@@ -2830,15 +2864,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lean(ScanArgs a, ListPlan pl) {
     DIAG(8, d_bounds);
     DIAG(9, d_admit);
     DIAG(10, 0);
-    // the partial lists' store operands, then the next item's fields (its record
-    // load is older than the stores and atomics below, so this waits for it alone)
-    int pr = it.pair[0];
-#pragma unroll
-    for (int g = 1; g < G; g++) pr = rg == g ? it.pair[g] : pr;
-    const int64_t slot = (int64_t)pr * 4 + wave;
-    const bool st = rg < it.cnt && re < k && !(pl.fault > 0 && slot % pl.fault == 1);  // (fault: test hook)
-    const int64_t beg = it.beg;
-    if (nxt >= 0) unpack(nrec);
+    // the next item's fields (without the prefetch: its record load is older than the
+    // stores and atomics below, so this waits for it alone), then this item's bounds
+    // and partial lists
+    if (!kScanPrefetch && nxt >= 0) unpack(nrec);
     publish();
     if (st) {
       const bool empty = rk == kKcNone;
