@@ -945,17 +945,28 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   float* xn = xs + dk * GQ;       // [GQ]
   f4 acc[NTL];
   const int i16 = lane & 15, k4 = lane >> 4;
-  if (d > 96 && d <= 128) {
+  // column i16 of tile t is centroid c0 + 16 t + i16, or with d <= 128 (the paired
+  // layout below) c0 + NTL i16 + t
+  const bool paired = d > 96 && d <= 128;
+  if (paired) {
     // (C1/C2, d = 128) every B row this wave uses is loaded before the queries
     // are staged, so the centroid loads overlap the staging and its barriers: one
-    // global round trip instead of a chain of chunk loads.  Same ascending-k MFMA
-    // chain as coarse_key_tile (rows past d clamped, their A entries 0).
+    // global round trip instead of a chain of chunk loads.  The two tiles take
+    // interleaved centroids, so a lane's two B values of a row are adjacent: one
+    // 8-byte load instead of two 4-byte ones (the 64 loads per lane of each key
+    // wave were queued ahead of every other load of the CU, r06 stamps).  Same
+    // ascending-k MFMA chain as coarse_key_tile (rows past d clamped, their A
+    // entries 0; columns past nlist read the zero padding of centT or are clamped,
+    // and never stored).
+    static_assert(NTL == 2, "paired B loads: two tiles per wave");
     float b[32][NTL];
+    const int cp2 = min(c0 + 2 * i16, ldc - 2);
 #pragma unroll
     for (int j = 0; j < 32; j++) {
       const int64_t kr = min(4 * j + k4, d - 1);
-#pragma unroll
-      for (int t = 0; t < NTL; t++) b[j][t] = centT[kr * ldc + min(c0 + t * 16 + i16, nlist - 1)];
+      const float2 v = *reinterpret_cast<const float2*>(centT + kr * ldc + cp2);
+      b[j][0] = v.x;
+      b[j][1] = v.y;
     }
     coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
     CDIAG(1);
@@ -976,7 +987,7 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   __syncthreads();  // xn
 #pragma unroll
   for (int t = 0; t < NTL; t++) {
-    const int c = c0 + t * 16 + i16;
+    const int c = paired ? c0 + NTL * i16 + t : c0 + t * 16 + i16;
     if (c >= nlist) continue;
     const float cnv = ip ? 0.f : cn[c];
 #pragma unroll
@@ -1171,9 +1182,13 @@ __device__ __forceinline__ float wave_ip_dis0(const float* __restrict__ xq, cons
   return -res;
 }
 
+// (IP a template parameter: the L2 instantiation carries no inner-product dis0 code --
+// these one-shot kernels' time is largely instruction fetch)
+template <int IP>
 __device__ __forceinline__ void coarse_emit(uint64_t run, int64_t q, int lane, int nprobe, float* __restrict__ out_dis,
-                                            int64_t* __restrict__ out_list, int ip, const float* __restrict__ x, int d,
+                                            int64_t* __restrict__ out_list, const float* __restrict__ x, int d,
                                             const CoarsePlan& cp) {
+  constexpr int ip = IP;
   const bool empty = run == kKcNone;
   const float rd = kc_key(run);
   const int64_t ri = empty ? kSentinelId : (int64_t)(uint32_t)run;
@@ -1233,11 +1248,11 @@ __device__ __forceinline__ uint64_t coarse_select_row(const float* row, int nlis
       p = lane < total ? scratch[lane] : kKcNone;
       kc_sort64(p, lane);
       kc_merge64(run, p, lane);
-    } else {  // many ties at the cut (rare): every 64-key slice of the block
-#pragma unroll
+    } else {  // many ties at the cut (rare): every 64-key slice of the block (a loop: compact code)
+#pragma unroll 1
       for (int u = 0; u < 16; u++) {
         const int c = base + u * 64 + lane;
-        p = c < nlist ? pack_kc(v[u], c) : kKcNone;
+        p = c < nlist ? pack_kc(row[c], c) : kKcNone;
         kc_sort64(p, lane);
         kc_merge64(run, p, lane);
       }
@@ -1247,9 +1262,10 @@ __device__ __forceinline__ uint64_t coarse_select_row(const float* row, int nlis
   return run;
 }
 
+template <int IP>
 __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__ keys, int64_t nq, int nlist,
                                                        int nprobe, float* __restrict__ out_dis,
-                                                       int64_t* __restrict__ out_list, int ip,
+                                                       int64_t* __restrict__ out_list,
                                                        const float* __restrict__ x, int d, CoarsePlan cp) {
   __shared__ uint64_t scratch[4][64];
   const int lane = threadIdx.x & 63;
@@ -1259,7 +1275,7 @@ __global__ __launch_bounds__(256) void k_coarse_select(const float* __restrict__
   SDIAG(0);
   const uint64_t run = coarse_select_row(keys + q * nlist, nlist, nprobe, scratch[wave], lane);
   SDIAG(3);
-  coarse_emit(run, q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
+  coarse_emit<IP>(run, q, lane, nprobe, out_dis, out_list, x, d, cp);
   SDIAG(5);
 }
 
@@ -2969,9 +2985,10 @@ __global__ __launch_bounds__(256) void k_coarse_segtop(const float* __restrict__
 
 // Per query (one wave): merge its nseg x nprobe segment candidates into the
 // final top-nprobe by (key, list), then emit and plan as k_coarse_select does.
+template <int IP>
 __global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __restrict__ cand, int64_t nq, int nseg,
                                                             int nprobe, float* __restrict__ out_dis,
-                                                            int64_t* __restrict__ out_list, int ip,
+                                                            int64_t* __restrict__ out_list,
                                                             const float* __restrict__ x, int d, CoarsePlan cp) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -2998,7 +3015,7 @@ __global__ __launch_bounds__(256) void k_coarse_select_cand(const uint64_t* __re
         tk.insert(mk, p[u], lane);
     }
   }
-  coarse_emit(tk.p[0], q, lane, nprobe, out_dis, out_list, ip, x, d, cp);
+  coarse_emit<IP>(tk.p[0], q, lane, nprobe, out_dis, out_list, x, d, cp);
 }
 
 // ---- stale partial lists: accounting, event log, repair
@@ -3961,6 +3978,10 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
   }
   hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
                      (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
+#ifdef DIAG_TWICE  // (diagnostic builds: the same launch again, warm; it rewrites the same values)
+  hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
+                     (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
+#endif
 }
 
 int coarse_segments(int64_t nq, int nlist, int d) {
@@ -4002,8 +4023,12 @@ void launch_coarse_segmented(const float* x, int64_t nq, int d, const float* cen
     cp.hi = hi;
     cp.cent = cent;
   }
-  hipLaunchKernelGGL(k_coarse_select_cand, dim3(nblocks(nq, 4)), dim3(256), 0, s, cand, nq, nseg, nprobe, out_dis,
-                     out_list, ip ? 1 : 0, x, d, cp);
+if (ip)
+      hipLaunchKernelGGL(k_coarse_select_cand<1>, dim3(nblocks(nq, 4)), dim3(256), 0, s, cand, nq, nseg, nprobe, out_dis,
+                     out_list, x, d, cp);
+  else
+      hipLaunchKernelGGL(k_coarse_select_cand<0>, dim3(nblocks(nq, 4)), dim3(256), 0, s, cand, nq, nseg, nprobe, out_dis,
+                     out_list, x, d, cp);
 }
 
 void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, float* out_dis, int64_t* out_list,
@@ -4019,8 +4044,12 @@ void launch_coarse_select(const float* keys, int64_t nq, int nlist, int nprobe, 
     cp.hi = hi;
     cp.cent = cent;
   }
-  hipLaunchKernelGGL(k_coarse_select, dim3(nblocks(nq, 4)), dim3(256), 0, s, keys, nq, nlist, nprobe, out_dis,
-                     out_list, ip ? 1 : 0, x, d, cp);
+  if (ip)
+    hipLaunchKernelGGL(k_coarse_select<1>, dim3(nblocks(nq, 4)), dim3(256), 0, s, keys, nq, nlist, nprobe, out_dis,
+                       out_list, x, d, cp);
+  else
+    hipLaunchKernelGGL(k_coarse_select<0>, dim3(nblocks(nq, 4)), dim3(256), 0, s, keys, nq, nlist, nprobe, out_dis,
+                       out_list, x, d, cp);
 }
 
 void launch_linear_transform(const float* x, int64_t n, int d_in, const float* AT, const float* b, int d_out, float* y,
@@ -4169,6 +4198,9 @@ static void launch_lists_MR(const ScanArgs& a, const ListPlan& pl, hipStream_t s
       hipLaunchKernelGGL(k_merge_big, dim3((unsigned)a.nq), dim3(64), 0, s, a, pl);
   }
   hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
+#ifdef DIAG_TWICE  // (diagnostic builds: the same merge again, warm; idempotent for k <= 64)
+  if (R == 1) hipLaunchKernelGGL(k_merge_probes<R>, dim3(nblocks(a.nq, 4)), dim3(256), 0, s, a, pl);
+#endif
 }
 
 template <int M>

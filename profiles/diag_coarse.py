@@ -40,7 +40,12 @@ def main():
         ix.search_device(xd, 10)
     torch.cuda.synchronize()
     fn(buf.ctypes.data, buf.nbytes)
-    ix.search_device(xd, 10)
+    mode = os.environ.get("MODE", "search")
+    if mode == "search":  # stamps of a search's coarse kernels (after the previous search's merge)
+        ix.search_device(xd, 10)
+    else:  # MODE=coarse2: the coarse step twice back to back, stamps of the second (warm start)
+        ix.coarse_device(xd)
+        ix.coarse_device(xd)
     torch.cuda.synchronize()
     assert fn(buf.ctypes.data, buf.nbytes) == 0
     full = buf.reshape(WG, ITEMS, SLOTS).astype(np.int64)
