@@ -100,11 +100,13 @@ def parse():
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=None,
                    help="batches in flight on that many HIP streams (step s on stream s %% N, each with its own "
-                        "workspace and, sharded, its own communicator; > 1 turns the index's batches-in-flight "
-                        "mode on so that consecutive batches overlap, DESIGN.md section 4); 1 = one batch at a "
-                        "time on one stream (also measured beside the value as ms_per_step_serial)")
+                        "workspace; > 1 turns the index's batches-in-flight mode on so that consecutive batches "
+                        "overlap, DESIGN.md section 4); 1 = one batch at a time on one stream (also measured beside "
+                        "the value as ms_per_step_serial).  Default: 2, or 3 in the shard flow (three compute "
+                        "streams + one RCCL communicator = the box's four hardware queues; r06 at world size 1: "
+                        "0.173 vs 0.185-0.201 ms per step with two)")
     return p.parse_args()
 
 
@@ -166,7 +168,7 @@ def main():
 
     xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
     k = args.k
-    inflight = max(1, args.inflight)
+    inflight = max(1, args.inflight if args.inflight is not None else (3 if shard else 2))
     ix.inflight = inflight > 1
     # Streams of the timed region, per process: `inflight` compute
     # streams, plus, sharded, the communicator streams of RCCL -- one communicator (the

@@ -4158,6 +4158,9 @@ int scan_lists_grid(int M, int k) {
   // workgroups per CU the LDS allows (LUTs, candidate queues, fused-plan prefix), at most 3
   const int lds = M * 256 * 4 * list_scan_group(M, k) + 4 * QCAP * 8 + 6 * kFusedPlanLists + 96;
   const int per_cu = std::max(1, std::min(3, 160 * 1024 / lds));
+#ifdef SCAN_GRID_QUARTERS  // (A/B builds: workgroups per CU in quarters, e.g. 7 = 1.75 per CU)
+  if (per_cu == 2) return std::max(8, (SCAN_GRID_QUARTERS * cus / 4 + 7) / 8 * 8);
+#endif
   return std::max(8, (per_cu * cus + 7) / 8 * 8);
 }
 
