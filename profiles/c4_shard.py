@@ -143,7 +143,7 @@ def main():
                                f"{ix.ntotal} vectors ({ix.ntotal * M / 1e9:.2f} GB codes), nprobe={nprobe}, k={k}, "
                                f"batch={B}", "shards": a.shards},
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": ach / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_scan_lists<48,1,1,2>",
+                     "frac": ach / HBM_PEAK_GBPS, "traffic": None, "kernel": "k_scan_lists<48,1,1,4>",
                      "alg_bytes_per_launch": bpl, "avg_launch_ms": avg},
         "add": {"vectors_generated": added, "kept": int(ix.ntotal), "seconds": t_add,
                 "vectors_per_s": added / t_add},
