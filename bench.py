@@ -96,7 +96,7 @@ def parse():
     p.add_argument("--event-every", type=int, default=5,
                    help="record the list-scan HIP events on every N-th timed step")
     p.add_argument("--no-recall", action="store_true")
-    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r05_scan_pmc.json"),
+    p.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r06_scan_pmc.json"),
                    help="counter-measured HBM bytes of the scan kernel; used only if its lib_sha256 matches "
                         "the library loaded now")
     p.add_argument("--no-extra", action="store_true", help="skip the k=100 and host-path search() rates")
