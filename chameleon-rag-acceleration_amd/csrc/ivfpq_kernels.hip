@@ -749,6 +749,9 @@ __device__ __forceinline__ void kc_merge64(uint64_t& run, uint64_t p, int lane) 
 // Workgroup = 16 queries x 256 centroids (wave w: 4 tiles of 16 centroids).
 // Workgroups past the key tiles build T3 [nq][M][256] (Faiss tree order) for
 // 16 queries x 1024 entries each, when T3out is set.
+#ifndef GEMM_AB
+#define GEMM_AB 0
+#endif
 constexpr int GQ = 16, GC = 128;
 
 // rows q0..q0+15 of x transposed into xs[dk][16] (k-major; zeros past nq and d)
@@ -891,6 +894,9 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   const int lane = tid & 63;
   const int wave = tid >> 6;
   CDIAG(0);
+#if GEMM_AB == 5  // diagnostic ablation: key workgroups exit at once
+  if ((int)blockIdx.x < ngemm) return;
+#endif
   if ((int)blockIdx.x >= ngemm) {
     // ---- T3 role: 16 queries x one sub-quantizer (256 entries, one per thread)
     const int tb = blockIdx.x - ngemm;
@@ -963,12 +969,22 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     const int cp2 = min(c0 + 2 * i16, ldc - 2);
 #pragma unroll
     for (int j = 0; j < 32; j++) {
+#if GEMM_AB == 2 || GEMM_AB == 4  // diagnostic ablation (profiles/r06_gemm_ab.sh): no centroid loads
+      b[j][0] = (float)(j + lane);
+      b[j][1] = (float)(j - lane);
+#else
       const int64_t kr = min(4 * j + k4, d - 1);
       const float2 v = *reinterpret_cast<const float2*>(centT + kr * ldc + cp2);
       b[j][0] = v.x;
       b[j][1] = v.y;
+#endif
     }
+#if GEMM_AB == 3 || GEMM_AB == 4  // diagnostic ablation: no query staging loads
+    for (int i = tid; i < dk * GQ + 2 * GQ; i += 256) xs[i] = 0.f;
+    __syncthreads();
+#else
     coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+#endif
     CDIAG(1);
 #pragma unroll
     for (int t = 0; t < NTL; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -994,6 +1010,9 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     for (int r = 0; r < 4; r++) {
       const int i = k4 * 4 + r;
       if (q0 + i >= nq) continue;
+#if GEMM_AB == 1  // diagnostic ablation: no key stores (kept alive by an impossible test)
+      if (acc[t][r] == 1.2345e37f)
+#endif
       keys[(q0 + i) * nlist + c] = coarse_key(acc[t][r], xn[i], cnv, ip);
     }
   }
