@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 
@@ -21,7 +22,7 @@ def main(pmc, trace, src, out):
             n = r["Kernel_Name"]
             if "k_scan_lists" not in n:
                 continue
-            n = n.split("(")[0].split("::")[-1]
+            n = re.search(r"k_\w+(<[^>]*>)?", n).group(0)
             first.setdefault(n, int(r.get("Dispatch_Id", 0) or 0))
             first[n] = min(first[n], int(r.get("Dispatch_Id", 0) or 0))
             per[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
