@@ -3415,9 +3415,11 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
   // every record and count read is tag-checked: a stale one sends the query to
   // k_merge_probes' full merge (which rescans its probe) instead of being used
   bool stale = false;
+  // (the tag test is a bitwise or, not a short-circuit: no branch per load, so
+  // independent loads stay in flight together)
   auto key_at = [&](int j, int i) __attribute__((always_inline)) {
     const uint2 v = *reinterpret_cast<const uint2*>(pl.part + (qb + j) * pl.ks + i);
-    stale = stale || !tag_ok(v.y, part_tag(pl.epoch, qb + j));
+    stale = stale | !tag_ok(v.y, part_tag(pl.epoch, qb + j));
     return __uint_as_float(v.x);
   };
 
@@ -3469,19 +3471,27 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
     __builtin_amdgcn_wave_barrier();
     const int S = carry, K2 = (k + r - 1) / r;
     if (S < K2) break;  // too few samples to bound (cannot happen for C > kBigCap, L <= 256)
-    uint32_t u[SV];
+    // sample positions first (LDS searches), then all SV loads at once (positions of
+    // absent samples clamped to entry 0 of list 0 and their keys dropped)
+    int sj[SV], si[SV];
 #pragma unroll
     for (int t = 0; t < SV; t++) {
       const int e = t * 64 + lane;
-      u[t] = 0xFFFFFFFFu;
-      if (e < S) {
-        int lo = 0, hi = 256;  // largest j with sp[j] <= e
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (sp[mid] <= e) lo = mid; else hi = mid;
-        }
-        u[t] = ukey_of(key_at(lo, (e - sp[lo] + 1) * r - 1));
+      int lo = 0, hi = 256;  // largest j with sp[j] <= e
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (sp[mid] <= e) lo = mid; else hi = mid;
       }
+      sj[t] = e < S ? lo : 0;
+      si[t] = e < S ? (e - sp[lo] + 1) * r - 1 : 0;
+    }
+    uint32_t u[SV];
+#pragma unroll
+    for (int t = 0; t < SV; t++) {
+      const uint2 v = *reinterpret_cast<const uint2*>(pl.part + (qb + sj[t]) * pl.ks + si[t]);
+      const bool ok = t * 64 + lane < S;  // (an absent sample's record is not tag-checked)
+      stale = stale | (ok & !tag_ok(v.y, part_tag(pl.epoch, qb + sj[t])));
+      u[t] = ok ? ukey_of(__uint_as_float(v.x)) : 0xFFFFFFFFu;
     }
     Tu = wave_kth_u32<SV>(u, K2);
     // each list's prefix <= Tu: an 8-ary search over its current prefix (7
@@ -3508,9 +3518,17 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
         lo = nlo;
         hi = nhi;
       }
+      // the last <= 8 entries: 8 unconditional loads (clamped into the list's slots;
+      // an absent entry's record is neither used nor tag-checked)
       uint32_t tail[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) tail[i] = lo + i < hi ? ukey_of(key_at(j, lo + i)) : 0xFFFFFFFFu;
+      for (int i = 0; i < 8; i++) {
+        const int ii = max(min(lo + i, hi - 1), 0);
+        const uint2 v = *reinterpret_cast<const uint2*>(pl.part + (qb + j) * pl.ks + ii);
+        const bool ok = lo + i < hi;
+        stale = stale | (ok & !tag_ok(v.y, part_tag(pl.epoch, qb + j)));
+        tail[i] = ok ? ukey_of(__uint_as_float(v.x)) : 0xFFFFFFFFu;
+      }
       int cnt = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) cnt += (lo + i < hi && tail[i] <= Tu) ? 1 : 0;
@@ -3544,7 +3562,7 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
           if (sp[mid] <= e) lo = mid; else hi = mid;
         }
         const uint4 r = pl.part[(qb + lo) * pl.ks + (e - sp[lo])];
-        stale = stale || !tag_ok(r.y, part_tag(pl.epoch, qb + lo));
+        stale = stale | !tag_ok(r.y, part_tag(pl.epoch, qb + lo));
         cd[e] = rec_key(r);
         cl[e] = rec_pos(r);
       }
@@ -3712,7 +3730,7 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
       const int j = div_small(e, ks, inv_k);
       if (e - j * ks < s_len[j]) {
         const uint2 v = *reinterpret_cast<const uint2*>(pr + e);  // (key, tag)
-        stale = stale || !tag_ok(v.y, part_tag(pl.epoch, qb + j));
+        stale = stale | !tag_ok(v.y, part_tag(pl.epoch, qb + j));
         key[u] = ukey_of(__uint_as_float(v.x));
       }
     }
@@ -3792,7 +3810,7 @@ __global__ __launch_bounds__(256) void k_merge_radix(ScanArgs a, ListPlan pl) {
     if (c && at < kRadixCap) {
       const int e = u * 256 + tid;
       const uint4 r = pr[e];
-      stale = stale || !tag_ok(r.y, part_tag(pl.epoch, qb + div_small(e, ks, inv_k)));
+      stale = stale | !tag_ok(r.y, part_tag(pl.epoch, qb + div_small(e, ks, inv_k)));
       cd[at] = rec_key(r);
       cl[at] = rec_pos(r);
     }

@@ -12,12 +12,12 @@ for v in ab0 ab1 ab2 ab3 ab4 ab5; do
   if [ $v = ab0 ]; then L=$R/chameleon-rag-acceleration_amd/lib/libivfpq.so; else L=$V/$v/libivfpq.so; fi
   IVFPQ_LIB=$L timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$v -o run -- python3 $R/profiles/gemm_ab.py 200 > $O/$v.log 2>&1 || { echo "$v failed"; tail -5 $O/$v.log; exit 1; }
   python3 - $O/$v/run_kernel_trace.csv $v <<'PY'
-import csv, sys, collections
+import csv, sys, collections, re
 g = collections.defaultdict(list)
 for r in csv.DictReader(open(sys.argv[1])):
     n = r['Kernel_Name']
     if 'k_coarse' in n or 'k_scan' in n or 'k_merge_probes' in n:
-        nm = n.split('(')[0].split('::')[-1] + ' grid ' + r['Grid_Size_X']
+        nm = re.search(r'k_\w+(<[^>]*>)?', n).group(0) + ' grid ' + r['Grid_Size_X']
         g[nm].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1000)
 for k, v in sorted(g.items()):
     v = sorted(v)

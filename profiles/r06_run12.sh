@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 R=$(pwd)
 O=gpurun_out/r06o
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_bigshapes.py -m gpu -x -q --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || { echo "gpu tests failed rc=$?"; tail -30 $O/gputest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_bigshapes.py tests/test_gpu_repair.py -m gpu -x -q --timeout 600 --timeout-method thread > $O/gputest.log 2>&1 || { echo "gpu tests failed rc=$?"; tail -30 $O/gputest.log; exit 1; }
 tail -1 $O/gputest.log
 B="--steps 40 --warmup 5 --no-cpu-baseline --no-recall --no-extra --no-peak"
 for rep in 1 2; do
