@@ -2168,6 +2168,10 @@ __global__ __launch_bounds__(256, 2) void k_scan_lists(ScanArgs a, ListPlan pl) 
 #pragma unroll
     for (int u = 0; u < NG; u++) {
       if (u + 1 < NG) fetch(u + 1, (u + 1) & 1);
+      // group u + 1's row loads stay issued ahead of group u's LUT stores: without this
+      // fence the compiler sank every row load next to its use, one round trip per
+      // element (16 in series per item at M = 64)
+      __asm__ volatile("" ::: "memory");
 #pragma unroll
       for (int e = 0; e < U; e++) {
         const int v = (u * U + e) * 256 + tid;
@@ -3520,11 +3524,14 @@ __global__ __launch_bounds__(64) void k_merge_big(ScanArgs a, ListPlan pl) {
       }
       // the last <= 8 entries: 8 unconditional loads (clamped into the list's slots;
       // an absent entry's record is neither used nor tag-checked)
+      // (lanes j >= L hold no list: their clamped loads read list L - 1's slot 0, inside
+      // this query's lists, never past the last query's)
+      const int jj = min(j, L - 1);
       uint32_t tail[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const int ii = max(min(lo + i, hi - 1), 0);
-        const uint2 v = *reinterpret_cast<const uint2*>(pl.part + (qb + j) * pl.ks + ii);
+        const uint2 v = *reinterpret_cast<const uint2*>(pl.part + (qb + jj) * pl.ks + ii);
         const bool ok = lo + i < hi;
         stale = stale | (ok & !tag_ok(v.y, part_tag(pl.epoch, qb + j)));
         tail[i] = ok ? ukey_of(__uint_as_float(v.x)) : 0xFFFFFFFFu;
