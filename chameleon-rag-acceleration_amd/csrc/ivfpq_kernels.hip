@@ -807,6 +807,37 @@ constexpr int NTL = GC / 64;  // 16 x 16 MFMA tiles per wave (32 centroids)
 // published by the caller's next barrier.
 __device__ __forceinline__ void coarse_stage_queries(float* xs, float* xn, const float* __restrict__ x, int64_t q0,
                                                      int64_t nq, int d, int dk, int tid) {
+#ifndef STAGE_LDS_NORM
+  if (d % 8 == 0 && dk == 128) {
+    // (C1/C2, d = 128) threads (i, j) = (tid >> 3, tid & 7), 128 of them: element
+    // k = j + 8 t of query row i for t < 16 -- loaded together, stored transposed
+    // (2-way bank conflicts instead of the float4 transpose's 32-way), and summed
+    // as the Faiss tree's sequential accumulator j; the 8 accumulators are folded
+    // by shuffles in the tree's order ((r4 + r0) + (r5 + r1)) + ((r6 + r2) + (r7 + r3)),
+    // fp adds being commutative, so no LDS round trip and one barrier
+    if (tid < GQ * 8) {
+      const int i = tid >> 3, j = tid & 7;
+      const float* xr = x + min(q0 + i, nq - 1) * d;
+      const bool qok = q0 + i < nq;
+      float v[16];
+#pragma unroll
+      for (int t = 0; t < 16; t++) v[t] = xr[min(j + 8 * t, d - 1)];
+      float acc8 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 16; t++) {
+        const float e = (qok && j + 8 * t < d) ? v[t] : 0.f;
+        xs[(j + 8 * t) * GQ + i] = e;
+        acc8 = acc8 + e * e;  // (a zero past d adds +0: the sum is unchanged)
+      }
+      const float s1 = acc8 + __shfl_xor(acc8, 4, 8);  // j < 4: r_j + r_{j+4}
+      const float s2 = s1 + __shfl_xor(s1, 1, 8);      // j = 0: h0, j = 2: h1
+      const float s3 = s2 + __shfl_xor(s2, 2, 8);      // j = 0: h0 + h1
+      if (j == 0) xn[i] = s3;
+    }
+    __syncthreads();
+    return;
+  }
+#endif
   fill_cols(xs, x, q0, nq, d, dk, tid);
   __syncthreads();
   // with d % 8 == 0 the 8 lane sums of each query are 8 independent sequential

@@ -1,21 +1,22 @@
-"""One-GPU emulation of bench.py's shard flow at N = 1, 2, 4, 8 (C2 index):
-per-rank times of rank 0 (lists [lo_0, hi_0) of a balanced N-way cut) for a
-global batch of 1024 x N queries.
+"""One-GPU emulation of bench.py's shard flow at N = 1, 2, 4, 8 (C2 index): the
+per-rank step of rank 0 (lists [lo_0, hi_0) of a balanced N-way cut) for a global
+batch of 1024 x N queries, in bench.py's r06 stream topology, with the collectives in
+the loop as real RCCL calls of the N-way payload on a one-rank nccl group:
 
-  coarse   : coarse_device on the rank's own 1024-query slice (flat in N)
-  preassigned: search_preassigned_device of the whole batch on the rank's lists
-               (plan + scan + merge; T3 for the batch is computed on a side stream
-               concurrently with the coarse step, as bench.py does), with the stage
-               split of a run without the side stream (ms): tables (T3, grows with
-               the batch), scan
-  merge    : merge_topk_device of the rank's slice over N partials
+  front (stream j of 3 in flight): coarse_tables_device (coarse of the own 1024-query
+        slice + T3 of the global batch, one launch), all_gather of N x 1024 x nprobe
+        probes, search_preassigned_device of the global batch on the rank's lists
+  back  (when stream j's next batch starts): all_to_all of the N x 1024 x k partials,
+        merge_topk_device of N partials of 1024 queries
 
-  step_wall_ms: the whole per-rank step by wall clock, one batch at a time and with two
-               batches in flight on two streams (as bench.py runs it)
+At world 1 the collectives copy to self, so their kernels and payloads are those of
+rank 0 of an N-way run but no xGMI transfer happens; the gathered probes are a stand-in
+(the full index's coarse result for the global batch is fed to the scan), so results are
+not checked here -- bench.py --shard-at-1 and the gloo / one-GPU shard tests check them.
 
-Collectives are not run (one GPU): their per-rank bytes are printed instead
-(all_gather of the probes: N x 1024 x nprobe x 12 B; all_to_all of partials:
-N x 1024 x k x 12 B).  Usage: python3 profiles/shard_emulation.py [--nb 1000000]
+Prints one JSON line per N: step_wall_ms (serial and 3 in flight), the stage split of
+the preassigned search, and the per-rank collective bytes.
+Usage: python3 profiles/shard_emulation.py [--nb 1000000] [--reps 10]
 """
 import argparse
 import json
@@ -33,12 +34,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nb", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--inflight", type=int, default=3)
     args = ap.parse_args()
     import torch
+    import torch.distributed as dist
 
     import faiss_amd as faiss
     from faiss_amd import datasets
-    from faiss_amd.sharding import balanced_list_ranges
+    from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    group = dist.group.WORLD
 
     k, B, npb = 10, 1024, 16
     xt = datasets.synthetic_sift_like(100_000, 128, seed=4321)
@@ -50,8 +59,6 @@ def main():
     full.nprobe = npb
     sizes = full.invlists.list_sizes()
     xd = torch.from_numpy(xq).cuda()
-    ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
-    out = []
     for N in (1, 2, 4, 8):
         lo, hi = balanced_list_ranges(sizes, N, 16)[0]
         sh = faiss.IndexIVFPQ(None, 128, 1024, 16, 8, device=0)
@@ -64,52 +71,50 @@ def main():
         sh.nprobe = npb
         xg = xd[:N * B]
         Dq_all, Iq_all = full.coarse_device(xg)  # stands in for the all-gathered probes
-        t = {"coarse": 0.0, "preassigned": 0.0, "merge": 0.0}
-        side = torch.cuda.Stream()
-        for rep in range(args.reps + 2):
-            e = [ev() for _ in range(4)]
-            e[0].record()
-            # T3 of the global batch on a side stream, concurrent with the coarse step (bench.py's shard flow)
-            side.wait_stream(torch.cuda.current_stream())
-            tok = sh.precompute_tables_device(xg, stream=side.cuda_stream)
-            sh.coarse_device(xg[:B])
-            e[1].record()
-            Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, tables=tok)
-            e[2].record()
-            faiss.merge_topk_device(torch.stack([Dp[:B]] * N), torch.stack([Ip[:B]] * N))
-            e[3].record()
-            torch.cuda.synchronize()
-            if rep >= 2:
-                t["coarse"] += e[0].elapsed_time(e[1]) / args.reps
-                t["preassigned"] += e[1].elapsed_time(e[2]) / args.reps
-                t["merge"] += e[2].elapsed_time(e[3]) / args.reps
-        # the whole per-rank step (T3 ahead on a side stream, coarse of the own slice,
-        # preassigned search, merge), wall clock over reps steps: one stream, then
-        # two batches in flight (step s on compute stream s % 2 with its own side stream)
-        comp = [torch.cuda.Stream() for _ in range(2)]
-        sides = [torch.cuda.Stream() for _ in range(2)]
+        streams = [torch.cuda.Stream() for _ in range(args.inflight)]
         outs = [(torch.empty((N * B, k), device="cuda"), torch.empty((N * B, k), dtype=torch.int64, device="cuda"))
-                for _ in range(2)]
+                for _ in range(args.inflight)]
+        pend = [None] * args.inflight
 
-        def rank_step(j):
-            with torch.cuda.stream(comp[j]):
-                sides[j].wait_stream(comp[j])
-                tok = sh.precompute_tables_device(xg, stream=sides[j].cuda_stream)
-                sh.coarse_device(xg[:B])
-                Dp, Ip = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j], tables=tok)
-                faiss.merge_topk_device(torch.stack([Dp[:B]] * N), torch.stack([Ip[:B]] * N))
+        def front(j):
+            with torch.cuda.stream(streams[j]):
+                _, _, tok = sh.coarse_tables_device(xg[:B], xg)
+                all_gather_probes(Dq_all, Iq_all, 1, group, force=True)  # N x B x nprobe payload
+                pend[j] = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j], tables=tok)
+
+        def back(j):
+            Dp, Ip = pend[j]
+            pend[j] = None
+            with torch.cuda.stream(streams[j]):
+                Ds, Is = exchange_partials(Dp, Ip, 1, group, force=True)  # N x B x k payload
+                faiss.merge_topk_device(Ds.view(N, B, k), Is.view(N, B, k))
+
+        def step(j):
+            if pend[j] is not None:
+                back(j)
+            front(j)
+
+        def drain():
+            for j in range(args.inflight):
+                if pend[j] is not None:
+                    back(j)
 
         wall = {}
-        for label, depth in (("serial", 1), ("inflight2", 2))[:2 if faiss.overlap_built() else 1]:
+        for label, depth in (("serial", 1), (f"inflight{args.inflight}", args.inflight)):
             sh.inflight = depth > 1
-            for s in range(4):
-                rank_step(s % depth)
+            for s in range(2 * depth):
+                step(s % depth)
+            drain()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for s in range(args.reps * 5):
-                rank_step(s % depth)
+                step(s % depth)
+                if depth == 1:
+                    drain()
+            drain()
             torch.cuda.synchronize()
             wall[label] = (time.perf_counter() - t0) * 1000.0 / (args.reps * 5)
+        sh.inflight = False
         sh.set_timing(True)
         for _ in range(args.reps):
             sh.search_preassigned_device(xg, k, Iq_all, Dq_all)
@@ -117,11 +122,11 @@ def main():
         sh.set_timing(False)
         st = sh.get_timing()
         split = {s: v[0] / max(v[1], 1) for s, v in st.items()}
-        row = {"N": N, "lists": [lo, hi], "batch": N * B, "ms": t, "step_wall_ms": wall,
-               "preassigned_stages_ms": split,
-               "allgather_bytes_per_rank": N * B * npb * 12, "alltoall_bytes_per_rank": N * B * k * 12}
+        row = {"N": N, "lists": [lo, hi], "batch": N * B, "step_wall_ms": wall, "preassigned_stages_ms": split,
+               "allgather_bytes_per_rank": N * B * npb * 12, "alltoall_bytes_per_rank": N * B * k * 12,
+               "collectives": "RCCL, one-rank nccl group (self-copies of the N-way payload)"}
         print(json.dumps(row), flush=True)
-        out.append(row)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":
