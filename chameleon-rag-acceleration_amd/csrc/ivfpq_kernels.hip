@@ -752,6 +752,12 @@ __device__ __forceinline__ void kc_merge64(uint64_t& run, uint64_t p, int lane) 
 #ifndef GEMM_AB
 #define GEMM_AB 0
 #endif
+// A/B switch (r06): cap k_coarse_gemm's VGPRs so its waves fit beside the scan's
+#ifdef GEMM_WAVES_PER_EU
+#define GEMM_VGPR_CAP __attribute__((amdgpu_waves_per_eu(GEMM_WAVES_PER_EU)))
+#else
+#define GEMM_VGPR_CAP
+#endif
 constexpr int GQ = 16, GC = 128;
 
 // rows q0..q0+15 of x transposed into xs[dk][16] (k-major; zeros past nq and d)
@@ -760,16 +766,11 @@ __device__ __forceinline__ void fill_cols(float* xs, const float* __restrict__ x
   if ((d & 3) == 0 && d <= 1024) {
     const int nk4 = dk / 4;  // thread k4: elements 4 k4 .. 4 k4 + 3 of the 16 rows
     for (int k4 = tid; k4 < nk4; k4 += 256) {
-      // the 16 loads are unconditional (clamped row and column) and zeroed after they
-      // land: as conditional loads the compiler put each in its own branch with an
-      // s_waitcnt vmcnt(0), 16 round trips in series (r06 ablation: 6.6 us of 18.5)
-      const int kc = min(k4, d / 4 - 1);
       float4 r[GQ];
 #pragma unroll
-      for (int i = 0; i < GQ; i++) r[i] = reinterpret_cast<const float4*>(x + min(q0 + i, nq - 1) * d)[kc];
-#pragma unroll
       for (int i = 0; i < GQ; i++)
-        if (!(q0 + i < nq && 4 * k4 < d)) r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        r[i] = (q0 + i < nq && 4 * k4 < d) ? reinterpret_cast<const float4*>(x + (q0 + i) * d)[k4]
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
       float4* row = reinterpret_cast<float4*>(xs + 4 * k4 * GQ);  // 4 k-rows of 16 floats
 #pragma unroll
       for (int i4 = 0; i4 < GQ / 4; i4++) {
@@ -801,58 +802,12 @@ struct CoarseT3 {
 typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int NTL = GC / 64;  // 16 x 16 MFMA tiles per wave (32 centroids)
 
-// Register-staged query tile (d % 8 == 0, dk == 128; C1/C2): threads (i, j) =
-// (tid >> 3, tid & 7), 128 of them, hold elements k = j + 8 t (t < 16) of query row i.
-// qtile_load issues the 16 loads; qtile_store writes them transposed into xs [128][16]
-// (2-way bank conflicts, where the float4 transpose of fill_cols had 32-way) and sums
-// them as the Faiss tree's sequential accumulator j; the 8 accumulators are folded by
-// shuffles in the tree's order ((r4 + r0) + (r5 + r1)) + ((r6 + r2) + (r7 + r3)) -- fp
-// adds are commutative -- so the norm needs no LDS round trip; ends with the barrier
-// that publishes xs and xn.  Split so that a caller can issue its own loads between
-// the two (k_coarse_gemm: the query rows first, then the centroid rows, so the staging
-// waits only for the former -- loads return in issue order).
-__device__ __forceinline__ void qtile_load(float (&v)[16], const float* __restrict__ x, int64_t q0, int64_t nq, int d,
-                                           int tid) {
-  // every thread loads (threads 128.. repeat rows 0..15: no divergent branch, so the
-  // compiler keeps the loads in flight across the caller's own loads)
-  const int i = (tid >> 3) & (GQ - 1), j = tid & 7;
-  const float* xr = x + min(q0 + i, nq - 1) * d;
-#pragma unroll
-  for (int t = 0; t < 16; t++) v[t] = xr[min(j + 8 * t, d - 1)];
-}
-__device__ __forceinline__ void qtile_store(const float (&v)[16], float* xs, float* xn, int64_t q0, int64_t nq, int d,
-                                            int tid, int gate = 1) {
-  const int i = (tid >> 3) & (GQ - 1), j = tid & 7;
-  const bool qok = gate && q0 + i < nq;
-  const bool mine = tid < GQ * 8;  // (threads 128.. computed duplicates: they store nothing)
-  float acc8 = 0.f;
-#pragma unroll
-  for (int t = 0; t < 16; t++) {
-    const float e = (qok && j + 8 * t < d) ? v[t] : 0.f;
-    if (mine) xs[(j + 8 * t) * GQ + i] = e;
-    acc8 = acc8 + e * e;  // (a zero past d adds +0: the sum is unchanged)
-  }
-  const float s1 = acc8 + __shfl_xor(acc8, 4, 8);  // j < 4: r_j + r_{j+4}
-  const float s2 = s1 + __shfl_xor(s1, 1, 8);      // j = 0: h0, j = 2: h1
-  const float s3 = s2 + __shfl_xor(s2, 2, 8);      // j = 0: h0 + h1
-  if (mine && j == 0) xn[i] = s3;
-  __syncthreads();
-}
-
 // Stage the A operand of a key tile (rows q0..q0+15 transposed, zero-padded to
 // dk) and |x_q|^2 in Faiss tree order into LDS (xs [dk][16], xn [16] + 128
 // floats of scratch).  Ends with the block barrier that publishes xs; xn is
 // published by the caller's next barrier.
 __device__ __forceinline__ void coarse_stage_queries(float* xs, float* xn, const float* __restrict__ x, int64_t q0,
                                                      int64_t nq, int d, int dk, int tid) {
-#ifndef STAGE_LDS_NORM
-  if (d % 8 == 0 && dk == 128) {
-    float v[16];
-    qtile_load(v, x, q0, nq, d, tid);
-    qtile_store(v, xs, xn, q0, nq, d, tid);
-    return;
-  }
-#endif
   fill_cols(xs, x, q0, nq, d, dk, tid);
   __syncthreads();
   // with d % 8 == 0 the 8 lane sums of each query are 8 independent sequential
@@ -936,7 +891,7 @@ __device__ __forceinline__ float coarse_key(float dot, float xn, float cn, int i
   return v < 0.f ? 0.f : v;
 }
 
-__global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
+__global__ __launch_bounds__(256) GEMM_VGPR_CAP void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
                                                      const float* __restrict__ centT, int ldc,
                                                      const float* __restrict__ cn, int nlist,
                                                      float* __restrict__ keys, int ip, int ngemm, CoarseT3 t3) {
@@ -1004,7 +959,11 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   const int i16 = lane & 15, k4 = lane >> 4;
   // column i16 of tile t is centroid c0 + 16 t + i16, or with d <= 128 (the paired
   // layout below) c0 + NTL i16 + t
+#ifdef GEMM_NO_PAIRED  // A/B switch (r06): the chunked B loads of coarse_key_tile (fewer VGPRs)
+  const bool paired = false;
+#else
   const bool paired = d > 96 && d <= 128;
+#endif
   if (paired) {
     // (C1/C2, d = 128) every B row this wave uses is loaded before the queries
     // are staged, so the centroid loads overlap the staging and its barriers: one
@@ -1016,13 +975,6 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
     // entries 0; columns past nlist read the zero padding of centT or are clamped,
     // and never stored).
     static_assert(NTL == 2, "paired B loads: two tiles per wave");
-    // the query rows are loaded first, the centroid rows after them: the staging then
-    // waits for its own 16 loads only, while the 32 centroid loads are still landing
-    const bool regtile = d % 8 == 0;  // (dk == 128 here)
-    float v[16];
-#if !(GEMM_AB == 3 || GEMM_AB == 4) && !defined(STAGE_LDS_NORM)
-    if (regtile) qtile_load(v, x, q0, nq, d, tid);
-#endif
     float b[32][NTL];
     const int cp2 = min(c0 + 2 * i16, ldc - 2);
 #pragma unroll
@@ -1037,22 +989,9 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
       b[j][1] = v.y;
 #endif
     }
-    // (keeps the centroid loads issued here, ahead of the staging's LDS stores and
-    // barrier: without it the compiler sank them below the barrier, next to the MFMAs)
-    __asm__ volatile("" ::: "memory");
-    // and the staging's arithmetic after them: `gate` (always 1) comes out of an asm
-    // the compiler cannot look through, so nothing that depends on it is hoisted above
-    // the centroid loads (their issue would otherwise wait for the query rows)
-    int gate = 1;
-    __asm__ volatile("" : "+v"(gate));
 #if GEMM_AB == 3 || GEMM_AB == 4  // diagnostic ablation: no query staging loads
     for (int i = tid; i < dk * GQ + 2 * GQ; i += 256) xs[i] = 0.f;
     __syncthreads();
-#elif !defined(STAGE_LDS_NORM)
-    if (regtile)
-      qtile_store(v, xs, xn, q0, nq, d, tid, gate);
-    else
-      coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
 #else
     coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
 #endif
