@@ -749,15 +749,6 @@ __device__ __forceinline__ void kc_merge64(uint64_t& run, uint64_t p, int lane) 
 // Workgroup = 16 queries x 256 centroids (wave w: 4 tiles of 16 centroids).
 // Workgroups past the key tiles build T3 [nq][M][256] (Faiss tree order) for
 // 16 queries x 1024 entries each, when T3out is set.
-#ifndef GEMM_AB
-#define GEMM_AB 0
-#endif
-// A/B switch (r06): cap k_coarse_gemm's VGPRs so its waves fit beside the scan's
-#ifdef GEMM_WAVES_PER_EU
-#define GEMM_VGPR_CAP __attribute__((amdgpu_waves_per_eu(GEMM_WAVES_PER_EU)))
-#else
-#define GEMM_VGPR_CAP
-#endif
 constexpr int GQ = 16, GC = 128;
 
 // rows q0..q0+15 of x transposed into xs[dk][16] (k-major; zeros past nq and d)
@@ -891,7 +882,7 @@ __device__ __forceinline__ float coarse_key(float dot, float xn, float cn, int i
   return v < 0.f ? 0.f : v;
 }
 
-__global__ __launch_bounds__(256) GEMM_VGPR_CAP void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
+__global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
                                                      const float* __restrict__ centT, int ldc,
                                                      const float* __restrict__ cn, int nlist,
                                                      float* __restrict__ keys, int ip, int ngemm, CoarseT3 t3) {
@@ -900,9 +891,6 @@ __global__ __launch_bounds__(256) GEMM_VGPR_CAP void k_coarse_gemm(const float* 
   const int lane = tid & 63;
   const int wave = tid >> 6;
   CDIAG(0);
-#if GEMM_AB == 5  // diagnostic ablation: key workgroups exit at once
-  if ((int)blockIdx.x < ngemm) return;
-#endif
   if ((int)blockIdx.x >= ngemm) {
     // ---- T3 role: 16 queries x one sub-quantizer (256 entries, one per thread)
     const int tb = blockIdx.x - ngemm;
@@ -957,72 +945,26 @@ __global__ __launch_bounds__(256) GEMM_VGPR_CAP void k_coarse_gemm(const float* 
   float* xn = xs + dk * GQ;       // [GQ]
   f4 acc[NTL];
   const int i16 = lane & 15, k4 = lane >> 4;
-  // column i16 of tile t is centroid c0 + 16 t + i16, or with d <= 128 (the paired
-  // layout below) c0 + NTL i16 + t
-#ifdef GEMM_NO_PAIRED  // A/B switch (r06): the chunked B loads of coarse_key_tile (fewer VGPRs)
-  const bool paired = false;
-#else
-  const bool paired = d > 96 && d <= 128;
-#endif
-  if (paired) {
-    // (C1/C2, d = 128) every B row this wave uses is loaded before the queries
-    // are staged, so the centroid loads overlap the staging and its barriers: one
-    // global round trip instead of a chain of chunk loads.  The two tiles take
-    // interleaved centroids, so a lane's two B values of a row are adjacent: one
-    // 8-byte load instead of two 4-byte ones (the 64 loads per lane of each key
-    // wave were queued ahead of every other load of the CU, r06 stamps).  Same
-    // ascending-k MFMA chain as coarse_key_tile (rows past d clamped, their A
-    // entries 0; columns past nlist read the zero padding of centT or are clamped,
-    // and never stored).
-    static_assert(NTL == 2, "paired B loads: two tiles per wave");
-    float b[32][NTL];
-    const int cp2 = min(c0 + 2 * i16, ldc - 2);
-#pragma unroll
-    for (int j = 0; j < 32; j++) {
-#if GEMM_AB == 2 || GEMM_AB == 4  // diagnostic ablation (profiles/r06_gemm_ab.sh): no centroid loads
-      b[j][0] = (float)(j + lane);
-      b[j][1] = (float)(j - lane);
-#else
-      const int64_t kr = min(4 * j + k4, d - 1);
-      const float2 v = *reinterpret_cast<const float2*>(centT + kr * ldc + cp2);
-      b[j][0] = v.x;
-      b[j][1] = v.y;
-#endif
-    }
-#if GEMM_AB == 3 || GEMM_AB == 4  // diagnostic ablation: no query staging loads
-    for (int i = tid; i < dk * GQ + 2 * GQ; i += 256) xs[i] = 0.f;
-    __syncthreads();
-#else
-    coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
-#endif
-    CDIAG(1);
-#pragma unroll
-    for (int t = 0; t < NTL; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 32; j++) {
-      const float av = xs[(4 * j + k4) * GQ + i16];
-#pragma unroll
-      for (int t = 0; t < NTL; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
-    }
-  } else {
-    coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
-    CDIAG(1);
-    coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
-  }
+  // B rows in 32-deep chunks, two in flight (coarse_key_tile).  r05-r06 loaded all 32 B
+  // rows of a wave up front (one round trip, 148 + 16 registers per lane): alone that
+  // was 1 us faster, but with batches in flight this launch runs in the other stream's
+  // scan tail, where a SIMD holding a 200-register scan wave fits one such wave and
+  // two of these (74 + 16): the two-in-flight step fell 0.128 -> 0.1145 ms (r06s,
+  // DESIGN.md section 4).  Keep this kernel's register footprint small.
+  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+  CDIAG(1);
+  coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
   CDIAG(2);
   __syncthreads();  // xn
 #pragma unroll
   for (int t = 0; t < NTL; t++) {
-    const int c = paired ? c0 + NTL * i16 + t : c0 + t * 16 + i16;
+    const int c = c0 + t * 16 + i16;
     if (c >= nlist) continue;
     const float cnv = ip ? 0.f : cn[c];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int i = k4 * 4 + r;
       if (q0 + i >= nq) continue;
-#if GEMM_AB == 1  // diagnostic ablation: no key stores (kept alive by an impossible test)
-      if (acc[t][r] == 1.2345e37f)
-#endif
       keys[(q0 + i) * nlist + c] = coarse_key(acc[t][r], xn[i], cnv, ip);
     }
   }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # coarse GEMM ablations (-DGEMM_AB=1..5: no key stores / no centroid loads / no query
-# staging / neither load / key workgroups exit at once): kernel durations by rocprofv3
+# staging / neither load / key workgroups exit at once): kernel durations by rocprofv3.
+# The switches lived in the paired-load path of commit 48d3133, removed after r06s.
 set -o pipefail
 cd "$(dirname "$0")/.."
 R=$(pwd)
