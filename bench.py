@@ -132,7 +132,7 @@ def main():
 
     import faiss_amd as faiss
     from faiss_amd import datasets
-    from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials
+    from faiss_amd.sharding import balanced_list_ranges, exchange_and_gather, exchange_partials
 
     t_setup = time.time()
     B = args.batch
@@ -198,18 +198,10 @@ def main():
     merged = {}
     pend = [None] * inflight  # sharded: the batch whose partials stream j has not exchanged yet
 
-    def front(b, j):
-        # coarse of this rank's slice + T3 of the global batch (one launch), probes
-        # all-gathered, this rank's lists scanned for the whole batch -- all on stream j
-        xg = xq_dev[b]
-        with torch.cuda.stream(streams[j]):
-            Dq_s, Iq_s, tok = ix.coarse_tables_device(xg[rank * B:(rank + 1) * B], xg)
-            Dq, Iq = all_gather_probes(Dq_s, Iq_s, world, groups[j], force=True)
-            Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j], tables=tok)
-        pend[j] = (b, Dp, Ip)
-
     def back(j):
-        # the partials of stream j's batch to their owners, merged on the GPU
+        # the partials of stream j's pending batch to their owners, merged on the GPU
+        # (the drain at the end of a timed region; in the loop the exchange rides with
+        # the next batch's all_gather, below)
         b, Dp, Ip = pend[j]
         pend[j] = None
         with torch.cuda.stream(streams[j]):
@@ -218,12 +210,23 @@ def main():
 
     def step(b, j=0):
         if shard:
-            # stream j's previous batch is exchanged first, then this batch's front half:
-            # on a shared communicator the order is ... all_gather(s-1), all_to_all(s-2),
-            # all_gather(s), ... so batch s waits only for batch s-2's scan, never s-1's
-            if pend[j] is not None:
-                back(j)
-            front(b, j)
+            # stream j: coarse of this rank's slice + T3 of the global batch (one
+            # launch); ONE collective launch that returns stream j's previous batch's
+            # partials to their owners and all-gathers this batch's probes; the previous
+            # batch's merge; this rank's lists scanned for the whole batch.  On a shared
+            # communicator every rank issues the same sequence, and batch s waits only
+            # for batch s - inflight's scan
+            prev = pend[j]
+            pend[j] = None
+            xg = xq_dev[b]
+            with torch.cuda.stream(streams[j]):
+                Dq_s, Iq_s, tok = ix.coarse_tables_device(xg[rank * B:(rank + 1) * B], xg)
+                Ds, Is, Dq, Iq = exchange_and_gather(prev[1] if prev else None, prev[2] if prev else None,
+                                                     Dq_s, Iq_s, world, groups[j], force=True)
+                if prev is not None:
+                    merged[prev[0]] = faiss.merge_topk_device(Ds, Is)
+                Dp, Ip = ix.search_preassigned_device(xg, k, Iq, Dq, Dbufs[j], Ibufs[j], tables=tok)
+            pend[j] = (b, Dp, Ip)
         else:  # stream j of the in-flight set, with its own output buffers
             ix.search_device(xq_dev[b], k, Dbufs[j], Ibufs[j], stream=streams[j].cuda_stream)
 

@@ -114,6 +114,40 @@ def all_gather_probes(Dq, Iq, world, group=None, force=False):
     return outD, outI
 
 
+def exchange_and_gather(Dp, Ip, Dq, Iq, world, group=None, force=False):
+    """One collective launch per shard step: the all_to_all of an earlier batch's
+    partials (exchange_partials) and the all_gather of this batch's probes
+    (all_gather_probes), issued together under one coalescing manager, so an RCCL
+    group holds the CUs once per step instead of twice.  ``Dp``/``Ip`` may be None
+    (no earlier batch pending).  Returns (Ds, Is, Dq_all, Iq_all); Ds/Is are None
+    when Dp is.  Every rank must call it with the same pattern of None (the
+    collectives are matched by order)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1 and not force:
+        Ds = Is = None
+        if Dp is not None:
+            Ds, Is = Dp.unsqueeze(0).clone(), Ip.unsqueeze(0).clone()
+        return Ds, Is, Dq, Iq
+    outD = torch.empty((world * Dq.shape[0], Dq.shape[1]), dtype=Dq.dtype, device=Dq.device)
+    outI = torch.empty((world * Iq.shape[0], Iq.shape[1]), dtype=Iq.dtype, device=Iq.device)
+    Dq, Iq = Dq.contiguous(), Iq.contiguous()
+    Ds = Is = None
+    with _coalesced(group, Dq.device):
+        if Dp is not None:
+            n, k = Dp.shape
+            B = n // world
+            Ds = torch.empty((world, B, k), dtype=Dp.dtype, device=Dp.device)
+            Is = torch.empty((world, B, k), dtype=Ip.dtype, device=Ip.device)
+            Dp, Ip = Dp.contiguous(), Ip.contiguous()
+            dist.all_to_all_single(Ds.view(world * B, k), Dp, group=group)
+            dist.all_to_all_single(Is.view(world * B, k), Ip, group=group)
+        dist.all_gather_into_tensor(outD, Dq, group=group)
+        dist.all_gather_into_tensor(outI, Iq, group=group)
+    return Ds, Is, outD, outI
+
+
 def merge_partials_reference(Ds, Is):
     """Host merge of [S, n, k] sorted partials by (distance, label); -1 labels last.
     Test reference for the device merge (faiss_amd.merge_topk_device)."""

@@ -3,11 +3,12 @@ per-rank step of rank 0 (lists [lo_0, hi_0) of a balanced N-way cut) for a globa
 batch of 1024 x N queries, in bench.py's r06 stream topology, with the collectives in
 the loop as real RCCL calls of the N-way payload on a one-rank nccl group:
 
-  front (stream j of 3 in flight): coarse_tables_device (coarse of the own 1024-query
-        slice + T3 of the global batch, one launch), all_gather of N x 1024 x nprobe
-        probes, search_preassigned_device of the global batch on the rank's lists
-  back  (when stream j's next batch starts): all_to_all of the N x 1024 x k partials,
-        merge_topk_device of N partials of 1024 queries
+  step (stream j of 3 in flight): coarse_tables_device (coarse of the own 1024-query
+        slice + T3 of the global batch, one launch); one collective launch with the
+        all_to_all of stream j's previous batch's N x 1024 x k partials and the
+        all_gather of this batch's N x 1024 x nprobe probes; merge_topk_device of the
+        previous batch's N partials; search_preassigned_device of the global batch on
+        the rank's lists
 
 At world 1 the collectives copy to self, so their kernels and payloads are those of
 rank 0 of an N-way run but no xGMI transfer happens; the gathered probes are a stand-in
@@ -41,7 +42,7 @@ def main():
 
     import faiss_amd as faiss
     from faiss_amd import datasets
-    from faiss_amd.sharding import all_gather_probes, balanced_list_ranges, exchange_partials
+    from faiss_amd.sharding import balanced_list_ranges, exchange_and_gather, exchange_partials
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
@@ -76,12 +77,6 @@ def main():
                 for _ in range(args.inflight)]
         pend = [None] * args.inflight
 
-        def front(j):
-            with torch.cuda.stream(streams[j]):
-                _, _, tok = sh.coarse_tables_device(xg[:B], xg)
-                all_gather_probes(Dq_all, Iq_all, 1, group, force=True)  # N x B x nprobe payload
-                pend[j] = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j], tables=tok)
-
         def back(j):
             Dp, Ip = pend[j]
             pend[j] = None
@@ -90,9 +85,17 @@ def main():
                 faiss.merge_topk_device(Ds.view(N, B, k), Is.view(N, B, k))
 
         def step(j):
-            if pend[j] is not None:
-                back(j)
-            front(j)
+            # bench.py's shard step: one collective launch carries stream j's previous
+            # batch's all_to_all (N x B x k) and this batch's all_gather (N x B x nprobe)
+            prev = pend[j]
+            pend[j] = None
+            with torch.cuda.stream(streams[j]):
+                _, _, tok = sh.coarse_tables_device(xg[:B], xg)
+                Ds, Is, _, _ = exchange_and_gather(prev[0] if prev else None, prev[1] if prev else None,
+                                                   Dq_all, Iq_all, 1, group, force=True)
+                if prev is not None:
+                    faiss.merge_topk_device(Ds.view(N, B, k), Is.view(N, B, k))
+                pend[j] = sh.search_preassigned_device(xg, k, Iq_all, Dq_all, *outs[j], tables=tok)
 
         def drain():
             for j in range(args.inflight):

@@ -123,7 +123,7 @@ def _collective_worker(rank, world, port, out):
     import torch
     import torch.distributed as dist
 
-    from faiss_amd.sharding import all_gather_probes, exchange_partials
+    from faiss_amd.sharding import all_gather_probes, exchange_and_gather, exchange_partials
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -156,6 +156,12 @@ def _collective_worker(rank, world, port, out):
         Ds2, Is2 = exchange_partials(Dp, Ip, world, grp)
         aD2, aI2 = all_gather_probes(Dq, Iq, world, grp)
         ok = ok and torch.equal(Ds2, Ds) and torch.equal(Is2, Is) and torch.equal(aD2, aD) and torch.equal(aI2, aI)
+    # bench.py's fused step exchange: the earlier batch's all_to_all and this batch's
+    # all_gather in one call (and the first step, with no earlier batch)
+    Ds3, Is3, aD3, aI3 = exchange_and_gather(Dp, Ip, Dq, Iq, world, groups[0])
+    ok = ok and torch.equal(Ds3, Ds) and torch.equal(Is3, Is) and torch.equal(aD3, aD) and torch.equal(aI3, aI)
+    n3 = exchange_and_gather(None, None, Dq, Iq, world)
+    ok = ok and n3[0] is None and n3[1] is None and torch.equal(n3[2], aD) and torch.equal(n3[3], aI)
     flags = [torch.zeros(1) for _ in range(world)]
     dist.all_gather(flags, torch.tensor([1.0 if ok else 0.0]))
     if rank == 0:
