@@ -796,7 +796,7 @@ struct ivfpq_index {
   // shard step: keys of this rank's slice, tables of the global batch, one launch)
   bool coarse_launch(const float* x, int64_t c, int np, float* dis, int64_t* lists, hipStream_t s,
                      const ListPlan* plan = nullptr, float* T3out = nullptr, const float* xt = nullptr,
-                     int64_t nt = 0) {
+                     int64_t nt = 0, bool hoist = false) {
     if (!xt) {
       xt = x;
       nt = c;
@@ -811,7 +811,7 @@ struct ivfpq_index {
     W().w_dist.ensure(sizeof(float) * c * nlist);
     W().w_qn.ensure(sizeof(float) * c);
     launch_coarse_keys(x, c, d, d_centT.as<float>(), d_cnorm.as<float>(), nlist, W().w_dist.as<float>(), s, ip(), T3out,
-                       d_cb.as<float>(), M, W().w_qn.as<float>(), xt, nt);
+                       d_cb.as<float>(), M, W().w_qn.as<float>(), xt, nt, hoist);
     if (np <= 64) {
       launch_coarse_select(W().w_dist.as<float>(), c, nlist, np, dis, lists, s, ip(), plan, d_off.as<int64_t>(), list_lo,
                            list_hi, x, d_cent.as<float>(), d);
@@ -865,7 +865,8 @@ struct ivfpq_index {
                           d_off.as<int64_t>(), list_lo, list_hi, ip(), true, k, plan, s);
       } else {
         planned =
-            coarse_launch(xq, c, np, W().w_dis0.as<float>(), W().w_lists.as<int64_t>(), s, &plan, W().w_T3.as<float>());
+            coarse_launch(xq, c, np, W().w_dis0.as<float>(), W().w_lists.as<int64_t>(), s, &plan, W().w_T3.as<float>(),
+                          nullptr, 0, /*hoist: the scan is not k_scan_lean*/ !(k <= 16 && M <= 16));
         lists = W().w_lists.as<int64_t>();
         if (!planned)
           launch_plan_count(lists, ip() ? nullptr : W().w_dis0.as<float>(), xq, d_cent.as<float>(), c, d, np,

@@ -37,13 +37,16 @@ struct ListPlan;
 // With T3out, the same launch builds T3 [nt][M][256] (Faiss tree order) of the
 // queries xt (nullable: the key tiles' own x, nq) -- the list-range shard step keys
 // its own slice and tabulates the whole global batch in one launch.
+// hoist: the key tiles load every centroid row up front (more registers, shorter
+// latency: for searches whose scan is not k_scan_lean).
 // xn_buf (nullable, [nq] floats of scratch): with d % 4 == 0, d >= 256 and nq >= 64
 // (coarse_tiled_ok) the keys come from 64-query x 128-centroid tiles with k-chunks
 // staged in LDS (|x|^2 from launch_row_norms into xn_buf), same arithmetic.
 bool coarse_tiled_ok(int d, int64_t nq);
 void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                         float* keys, hipStream_t s, bool ip, float* T3out = nullptr, const float* cb = nullptr,
-                        int M = 0, float* xn_buf = nullptr, const float* xt = nullptr, int64_t nt = 0);
+                        int M = 0, float* xn_buf = nullptr, const float* xt = nullptr, int64_t nt = 0,
+                        bool hoist = false);
 // Per query the nprobe (<= 64) smallest (key, list) pairs of a key matrix;
 // out_dis receives the quantizer's distances (L2) or similarities (IP).  With
 // `plan`, the epilogue also plans the batch (first usable probe, tau reset,

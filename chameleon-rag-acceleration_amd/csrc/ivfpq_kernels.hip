@@ -882,6 +882,7 @@ __device__ __forceinline__ float coarse_key(float dot, float xn, float cn, int i
   return v < 0.f ? 0.f : v;
 }
 
+template <int HOIST>
 __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x, int64_t nq, int d,
                                                      const float* __restrict__ centT, int ldc,
                                                      const float* __restrict__ cn, int nlist,
@@ -945,20 +946,50 @@ __global__ __launch_bounds__(256) void k_coarse_gemm(const float* __restrict__ x
   float* xn = xs + dk * GQ;       // [GQ]
   f4 acc[NTL];
   const int i16 = lane & 15, k4 = lane >> 4;
-  // B rows in 32-deep chunks, two in flight (coarse_key_tile).  r05-r06 loaded all 32 B
-  // rows of a wave up front (one round trip, 148 + 16 registers per lane): alone that
-  // was 1 us faster, but with batches in flight this launch runs in the other stream's
-  // scan tail, where a SIMD holding a 200-register scan wave fits one such wave and
-  // two of these (74 + 16): the two-in-flight step fell 0.128 -> 0.1145 ms (r06s,
-  // DESIGN.md section 4).  Keep this kernel's register footprint small.
-  coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
-  CDIAG(1);
-  coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
+  // B rows: HOIST = 0 (searches whose scan is k_scan_lean) in 32-deep chunks, two in
+  // flight (coarse_key_tile), 74 + 16 registers per lane; HOIST = 1 (every other
+  // search, d in (96, 128]) every B row of the wave up front, 148 + 16.  With batches in
+  // flight this launch runs in the other stream's scan tail: beside the lean scan's
+  // 200-register waves a SIMD fits two HOIST = 0 waves and one HOIST = 1 wave, and the
+  // chunked form took the C2 two-in-flight step from 0.128 to 0.1145 ms (r06s); beside
+  // k_scan_lists (k > 16: 236 registers) nothing fits, and the up-front loads' shorter
+  // latency wins (r05: k = 100 4.74 -> 5.07 M queries/s).  DESIGN.md section 4.
+  const bool paired = HOIST && d > 96 && d <= 128;
+  if (paired) {
+    // the two tiles take interleaved centroids, so a lane's two B values of a row are
+    // adjacent: one 8-byte load.  Same ascending-k MFMA chain as coarse_key_tile (rows
+    // past d clamped, their A entries 0; columns past nlist read the zero padding of
+    // centT or are clamped, and never stored)
+    static_assert(NTL == 2, "paired B loads: two tiles per wave");
+    float b[32][NTL];
+    const int cp2 = min(c0 + 2 * i16, ldc - 2);
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const int64_t kr = min(4 * j + k4, d - 1);
+      const float2 v = *reinterpret_cast<const float2*>(centT + kr * ldc + cp2);
+      b[j][0] = v.x;
+      b[j][1] = v.y;
+    }
+    coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+    CDIAG(1);
+#pragma unroll
+    for (int t = 0; t < NTL; t++) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+      const float av = xs[(4 * j + k4) * GQ + i16];
+#pragma unroll
+      for (int t = 0; t < NTL; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[j][t], acc[t], 0, 0, 0);
+    }
+  } else {
+    coarse_stage_queries(xs, xn, x, q0, nq, d, dk, tid);
+    CDIAG(1);
+    coarse_key_tile(acc, xs, GQ, 0, centT, ldc, nlist, d, dk, c0, lane);
+  }
   CDIAG(2);
   __syncthreads();  // xn
 #pragma unroll
   for (int t = 0; t < NTL; t++) {
-    const int c = c0 + t * 16 + i16;
+    const int c = paired ? c0 + NTL * i16 + t : c0 + t * 16 + i16;
     if (c >= nlist) continue;
     const float cnv = ip ? 0.f : cn[c];
 #pragma unroll
@@ -3941,8 +3972,11 @@ bool coarse_tiled_ok(int d, int64_t nq) { return d % 4 == 0 && d >= 256 && nq >=
 
 void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, const float* cn, int nlist,
                         float* keys, hipStream_t s, bool ip, float* T3out, const float* cb, int M, float* xn_buf,
-                        const float* xt, int64_t nt) {
+                        const float* xt, int64_t nt, bool hoist) {
   if (nq <= 0) return;
+#ifdef COARSE_NO_HOIST  // A/B switch (r06)
+  hoist = false;
+#endif
   if (!xt) {  // T3 of the key tiles' own queries
     xt = x;
     nt = nq;
@@ -3974,16 +4008,17 @@ void launch_coarse_keys(const float* x, int64_t nq, int d, const float* centT, c
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (dev < 64 && !(attr_done & (1ull << dev))) {
-      (void)hipFuncSetAttribute((const void*)k_coarse_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_coarse_gemm<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_coarse_gemm<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       attr_done |= 1ull << dev;
     }
   }
-  hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
-                     (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
-#ifdef DIAG_TWICE  // (diagnostic builds: the same launch again, warm; it rewrites the same values)
-  hipLaunchKernelGGL(k_coarse_gemm, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
-                     (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
-#endif
+  if (hoist)
+    hipLaunchKernelGGL(k_coarse_gemm<1>, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
+                       (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
+  else
+    hipLaunchKernelGGL(k_coarse_gemm<0>, dim3((unsigned)(ngemm + t3.nblk)), dim3(256), smem, s, x, nq, d, centT,
+                       (nlist + 3) & ~3, cn, nlist, keys, ip ? 1 : 0, ngemm, t3);
 }
 
 int coarse_segments(int64_t nq, int nlist, int d) {
