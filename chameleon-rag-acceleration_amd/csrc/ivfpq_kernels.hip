@@ -4198,7 +4198,15 @@ int scan_lists_grid(int M, int k) {
 #ifdef SCAN_GRID_QUARTERS  // (A/B builds: workgroups per CU in quarters, e.g. 7 = 1.75 per CU)
   if (per_cu == 2) return std::max(8, (SCAN_GRID_QUARTERS * cus / 4 + 7) / 8 * 8);
 #endif
-  return std::max(8, (per_cu * cus + 7) / 8 * 8);
+  // IVFPQ_SCAN_FREE_CUS (performance only, default 0): the persistent scan is sized for
+  // that many CUs fewer, so kernels of other streams -- RCCL's collectives in the shard
+  // flow -- find room while a scan runs instead of waiting for its tail
+  static int free_cus = -1;
+  if (free_cus < 0) {
+    const char* e = getenv("IVFPQ_SCAN_FREE_CUS");
+    free_cus = e ? std::max(0, std::min(atoi(e), cus / 2)) : 0;
+  }
+  return std::max(8, (per_cu * (cus - free_cus) + 7) / 8 * 8);
 }
 
 int device_cus() {
