@@ -302,6 +302,7 @@ def main():
     # the same steps one batch at a time on one stream (reported beside the value)
     serial_ms, stages_serial = None, None
     if inflight > 1:
+        ix.inflight = False  # one batch at a time: the handle's serial mode (full scan grid)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for s in range(args.steps):
@@ -318,6 +319,7 @@ def main():
     torch.cuda.synchronize()
     ix.set_timing(False)
     stage_split = ix.get_timing()
+    ix.inflight = inflight > 1
 
     # extra rates (rank 0 view, untimed by the contract): k = 100 (the reference's
     # profiling K) on the device path, and the host-buffer search() (PCIe included)

@@ -163,6 +163,8 @@ constexpr int kSegmentedNlist = 8192;
 // on, device searches on different streams overlap, each on its own per-stream
 // workspace; off, a search is ordered after every search still in flight on
 // another stream.  IVFPQ_INFLIGHT=1 in the environment turns it on for new handles.
+constexpr int kInflightFreeCus = 16;
+
 bool inflight_default() {
   const char* e = std::getenv("IVFPQ_INFLIGHT");
   return e && e[0] == '1';
@@ -286,14 +288,18 @@ struct ivfpq_index {
     }
   }
 
-  ListPlan make_plan(int64_t nq, int np, int k, hipStream_t s) {
+  ListPlan make_plan(int64_t nq, int np, int k, hipStream_t s, bool leave_free = false) {
     const int nloc = std::max(list_hi - list_lo, 1);
     Work& w = W();
     const int G = list_scan_group(M, k);
     ListPlan pl;
     pl.cap = (int)nq;
     pl.max_items = list_scan_max_items(nq * np, nloc, G);
-    pl.grid = scan_lists_grid(M, k);
+    // leave_free (a full search with batches in flight): the scan leaves kInflightFreeCus
+    // CUs to the other streams' coarse and merge kernels (r06x sweep: C2 step -2.5 %;
+    // DESIGN.md section 4); one batch at a time, and in the shard flow's preassigned
+    // searches, where the sweep was inconclusive, it takes them all
+    pl.grid = scan_lists_grid(M, k, leave_free ? kInflightFreeCus : 0);
     if (!w.p_cnt.p || w.p_cnt.bytes < sizeof(int32_t) * 2 * nloc) {
       // kept zero between batches by k_scan_lists; zeroed once here
       w.p_cnt.ensure(sizeof(int32_t) * 2 * nloc);
@@ -855,7 +861,7 @@ struct ivfpq_index {
     for (int64_t q0 = 0; q0 < n; q0 += qc) {
       const int64_t c = std::min(qc, n - q0);
       const float* xq = x + q0 * d;
-      const ListPlan plan = make_plan(c, np, k, s);
+      const ListPlan plan = make_plan(c, np, k, s, inflight && !preassigned);
       const int64_t* lists;
       bool planned = false;
       const int tm = mark_begin(ST_COARSE, s);

@@ -166,7 +166,7 @@ bool scan_fused_plan(int nloc, int max_items, int M);
 
 int list_scan_group(int M, int k);  // pairs per work item (G) used for (M, k)
 int list_scan_max_items(int64_t npairs, int nloc, int G);
-int scan_lists_grid(int M, int k);  // persistent grid size for the device (2-3 workgroups per CU by LDS)
+int scan_lists_grid(int M, int k, int free_cus = 0);  // persistent grid (2-3 workgroups per CU by LDS) on all but free_cus CUs
 bool scan_supported_M(int M);
 // list scan + probe merge; ev_lists (nullable): two events recorded around the list-scan kernel alone
 void launch_scan_lists(const ScanArgs& a, const ListPlan& plan, hipStream_t s, hipEvent_t* ev_lists = nullptr);

@@ -4185,7 +4185,7 @@ int list_scan_max_items(int64_t npairs, int nloc, int G) {
   return (int)v;
 }
 
-int scan_lists_grid(int M, int k) {
+int scan_lists_grid(int M, int k, int free_cus) {
   static int cus = 0;
   if (!cus) {
     int dev = 0, n = 256;
@@ -4198,14 +4198,17 @@ int scan_lists_grid(int M, int k) {
 #ifdef SCAN_GRID_QUARTERS  // (A/B builds: workgroups per CU in quarters, e.g. 7 = 1.75 per CU)
   if (per_cu == 2) return std::max(8, (SCAN_GRID_QUARTERS * cus / 4 + 7) / 8 * 8);
 #endif
-  // IVFPQ_SCAN_FREE_CUS (performance only, default 0): the persistent scan is sized for
-  // that many CUs fewer, so kernels of other streams -- RCCL's collectives in the shard
-  // flow -- find room while a scan runs instead of waiting for its tail
-  static int free_cus = -1;
-  if (free_cus < 0) {
+  // free_cus: the persistent scan is sized for that many CUs fewer, so kernels of other
+  // streams (the next batch's coarse step and merge, RCCL's collectives in the shard
+  // flow) find room while a scan runs instead of waiting for its tail.  Performance
+  // only; IVFPQ_SCAN_FREE_CUS overrides it (A/B runs)
+  static int env_free = -2;
+  if (env_free == -2) {
     const char* e = getenv("IVFPQ_SCAN_FREE_CUS");
-    free_cus = e ? std::max(0, std::min(atoi(e), cus / 2)) : 0;
+    env_free = e ? std::max(0, atoi(e)) : -1;
   }
+  if (env_free >= 0) free_cus = env_free;
+  free_cus = std::max(0, std::min(free_cus, cus / 2));
   return std::max(8, (per_cu * (cus - free_cus) + 7) / 8 * 8);
 }
 
