@@ -104,10 +104,11 @@ def parse():
                    help="batches in flight on that many HIP streams (step s on stream s %% N, each with its own "
                         "workspace; > 1 turns the index's batches-in-flight mode on so that consecutive batches "
                         "overlap, DESIGN.md section 4); 1 = one batch at a time on one stream (also measured beside "
-                        "the value as ms_per_step_serial).  Default: 2 (the shard flow then holds two compute "
-                        "streams + one RCCL communicator, within the box's four hardware queues; r06 at world "
-                        "size 1 with one collective launch per step: 0.169 ms per step with two, 0.166-0.196 "
-                        "with three, 0.176-0.227 with four; plain: 0.109 / 0.123 / 0.110)")
+                        "the value as ms_per_step_serial).  Default: 2, or 3 in the shard flow (three compute "
+                        "streams + one RCCL communicator = the box's four hardware queues); DESIGN.md section 5 "
+                        "has the depth A/Bs (plain: 0.109 / 0.123 / 0.110 ms with 2 / 3 / 4; shard flow at world "
+                        "size 1: noisy, 0.14-0.20 ms with 3 and 0.17-0.19 with 2; one-GPU emulation at N = 2-8: "
+                        "3 at or below 2)")
     return p.parse_args()
 
 
@@ -169,7 +170,7 @@ def main():
 
     xq_dev = torch.from_numpy(xq).to(dev).view(args.nbatches, Bg, args.d)
     k = args.k
-    inflight = max(1, args.inflight if args.inflight is not None else 2)
+    inflight = max(1, args.inflight if args.inflight is not None else (3 if shard else 2))
     ix.inflight = inflight > 1
     # Streams of the timed region, per process: `inflight` compute
     # streams, plus, sharded, the communicator streams of RCCL -- one communicator (the

@@ -3,7 +3,7 @@ per-rank step of rank 0 (lists [lo_0, hi_0) of a balanced N-way cut) for a globa
 batch of 1024 x N queries, in bench.py's r06 stream topology, with the collectives in
 the loop as real RCCL calls of the N-way payload on a one-rank nccl group:
 
-  step (stream j of 2 in flight): coarse_tables_device (coarse of the own 1024-query
+  step (stream j of 3 in flight): coarse_tables_device (coarse of the own 1024-query
         slice + T3 of the global batch, one launch); one collective launch with the
         all_to_all of stream j's previous batch's N x 1024 x k partials and the
         all_gather of this batch's N x 1024 x nprobe probes; merge_topk_device of the
@@ -15,7 +15,7 @@ rank 0 of an N-way run but no xGMI transfer happens; the gathered probes are a s
 (the full index's coarse result for the global batch is fed to the scan), so results are
 not checked here -- bench.py --shard-at-1 and the gloo / one-GPU shard tests check them.
 
-Prints one JSON line per N: step_wall_ms (serial and 2 in flight), the stage split of
+Prints one JSON line per N: step_wall_ms (serial and 3 in flight), the stage split of
 the preassigned search, and the per-rank collective bytes.
 Usage: python3 profiles/shard_emulation.py [--nb 1000000] [--reps 10]
 """
@@ -35,7 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nb", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=3)
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
