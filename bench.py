@@ -85,6 +85,9 @@ def parse():
                    help="run the list-range shard flow at WORLD_SIZE=1 too, with a real nccl (RCCL) process group of "
                         "one rank: every collective of the N > 1 step is a real RCCL call and its communicator stream "
                         "exists (the stream topology the scaling run uses, measured on one GPU)")
+    p.add_argument("--rccl-priority", choices=["normal", "high"], default="normal",
+                   help="shard flow: priority of RCCL's communicator stream (high: its collective kernels are "
+                        "dispatched ahead of the compute streams' pending workgroups)")
     p.add_argument("--comms", choices=["one", "per-stream"], default="one",
                    help="shard flow: one communicator for every in-flight stream (default; the loop issues each "
                         "batch's all_to_all after the next batch's all_gather, so the communicator's stream never "
@@ -130,7 +133,12 @@ def main():
             os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 2000))
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rccl_priority == "high":
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=dev, pg_options=opts)
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import faiss_amd as faiss
     from faiss_amd import datasets
