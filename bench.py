@@ -85,6 +85,8 @@ def parse():
                    help="run the list-range shard flow at WORLD_SIZE=1 too, with a real nccl (RCCL) process group of "
                         "one rank: every collective of the N > 1 step is a real RCCL call and its communicator stream "
                         "exists (the stream topology the scaling run uses, measured on one GPU)")
+    p.add_argument("--stream-priority", choices=["normal", "high"], default="normal",
+                   help="priority of the in-flight compute streams (high: ahead of RCCL's communicator stream)")
     p.add_argument("--rccl-priority", choices=["normal", "high"], default="normal",
                    help="shard flow: priority of RCCL's communicator stream (high: its collective kernels are "
                         "dispatched ahead of the compute streams' pending workgroups)")
@@ -190,7 +192,7 @@ def main():
                   else [dist.group.WORLD] * inflight)
     else:
         groups = None
-    streams = [torch.cuda.Stream(dev) for _ in range(inflight)]
+    streams = [torch.cuda.Stream(dev, priority=-1 if args.stream_priority == "high" else 0) for _ in range(inflight)]
     Dbufs = [torch.empty((Bg, k), dtype=torch.float32, device=dev) for _ in range(inflight)]
     Ibufs = [torch.empty((Bg, k), dtype=torch.int64, device=dev) for _ in range(inflight)]
     Dbuf, Ibuf = Dbufs[0], Ibufs[0]
